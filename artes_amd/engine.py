@@ -1,0 +1,152 @@
+"""ctypes binding of the HIP transport engine (``artes_amd/lib/libartes_hip.so``).
+
+This is the product path: every packet is transported by the gfx950 kernel behind
+``include/artes_amd.h``.  There is deliberately no CPU fallback -- if the shared
+library is missing or no device is visible, :class:`EngineUnavailable` is raised.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .abi import ARTES_NUM_COUNTERS, ARTES_NUM_ERR, COUNTER_NAMES, GridArrays, GridDesc, RunParams
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libartes_hip.so")
+
+_lib = None
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineUnavailable(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    L.artes_abi_version.restype = C.c_int32
+    L.artes_build_info.restype = C.c_char_p
+    L.artes_last_error.restype = C.c_char_p
+    L.artes_device_count.restype = C.c_int32
+    L.artes_grid_create.restype = C.c_int32
+    L.artes_grid_create.argtypes = [C.POINTER(GridDesc), C.c_int32, C.POINTER(C.c_void_p)]
+    L.artes_grid_destroy.argtypes = [C.c_void_p]
+    L.artes_grid_cell_depth.restype = C.c_int32
+    L.artes_grid_cell_depth.argtypes = [C.c_void_p, C.c_int32]
+    L.artes_grid_num_matrices.restype = C.c_int32
+    L.artes_grid_num_matrices.argtypes = [C.c_void_p]
+    dp, up = C.POINTER(C.c_double), C.POINTER(C.c_uint64)
+    L.artes_run.restype = C.c_int32
+    L.artes_run.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64, dp, dp, up, up]
+    L.artes_run_device.restype = C.c_int32
+    L.artes_run_device.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64,
+                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.artes_run_trace.restype = C.c_int32
+    L.artes_run_trace.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64, dp]
+    L.artes_last_kernel_ms.restype = C.c_double
+    L.artes_last_kernel_ms.argtypes = [C.c_void_p]
+    if L.artes_abi_version() != 1:
+        raise EngineUnavailable("ABI version mismatch")
+    _lib = L
+    return L
+
+
+def device_count() -> int:
+    return lib().artes_device_count()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise EngineError(f"{what} failed ({rc}): {lib().artes_last_error().decode(errors='replace')}")
+
+
+class RunResult:
+    """Raw (un-normalised) outputs of one transport call."""
+
+    def __init__(self, det, totals, counters, err):
+        self.det = det            # [4][4][ny][nx]
+        self.totals = totals      # [8]
+        self.counters = counters  # [ARTES_NUM_COUNTERS]
+        self.err = err            # [ARTES_NUM_ERR]
+
+    def counter(self, name: str) -> int:
+        return int(self.counters[COUNTER_NAMES.index(name)])
+
+    def __iadd__(self, other: "RunResult"):
+        self.det += other.det
+        self.totals += other.totals
+        self.counters += other.counters
+        self.err += other.err
+        return self
+
+
+class Grid:
+    """Device-resident atmosphere tables (``artes_grid_create``)."""
+
+    def __init__(self, atm: dict, device: int = 0, oblateness: float = 0.0):
+        L = lib()
+        n = L.artes_device_count()
+        if n <= 0:
+            raise EngineUnavailable("no HIP device visible")
+        self.arrays = GridArrays(atm, oblateness)
+        self.h = C.c_void_p()
+        self.device = device
+        _check(L.artes_grid_create(C.byref(self.arrays.desc), device, C.byref(self.h)), "artes_grid_create")
+        # the host copies are not needed once the tables live in HBM
+        self.nr, self.ntheta, self.nphi, self.nwav = (self.arrays.nr, self.arrays.ntheta, self.arrays.nphi,
+                                                      self.arrays.nwav)
+        self.arrays = None
+
+    def cell_depth(self, wl: int = 0) -> int:
+        return lib().artes_grid_cell_depth(self.h, wl)
+
+    def num_matrices(self) -> int:
+        return lib().artes_grid_num_matrices(self.h)
+
+    def run(self, params: RunParams, first: int, n: int, seed: int) -> RunResult:
+        det = np.zeros((4, 4, params.ny, params.nx))
+        tot = np.zeros(8)
+        cnt = np.zeros(ARTES_NUM_COUNTERS, dtype=np.uint64)
+        err = np.zeros(ARTES_NUM_ERR, dtype=np.uint64)
+        dp, up = C.POINTER(C.c_double), C.POINTER(C.c_uint64)
+        _check(lib().artes_run(self.h, C.byref(params), int(first), int(n), int(seed), det.ctypes.data_as(dp),
+                               tot.ctypes.data_as(dp), cnt.ctypes.data_as(up), err.ctypes.data_as(up)), "artes_run")
+        return RunResult(det, tot, cnt, err)
+
+    def run_device(self, params: RunParams, first: int, n: int, seed: int, det_ptr: int, tot2_ptr: int = 0,
+                   cnt_ptr: int = 0, err_ptr: int = 0, stream: int = 0) -> None:
+        """Asynchronous launch accumulating into device buffers (e.g. torch tensors' data_ptr())."""
+        _check(lib().artes_run_device(self.h, C.byref(params), int(first), int(n), int(seed), C.c_void_p(det_ptr),
+                                      C.c_void_p(tot2_ptr or None), C.c_void_p(cnt_ptr or None),
+                                      C.c_void_p(err_ptr or None), C.c_void_p(stream or None)), "artes_run_device")
+
+    def trace(self, params: RunParams, first: int, n: int, seed: int) -> np.ndarray:
+        rec = np.zeros((n, 4))
+        _check(lib().artes_run_trace(self.h, C.byref(params), int(first), int(n), int(seed),
+                                     rec.ctypes.data_as(C.POINTER(C.c_double))), "artes_run_trace")
+        return rec
+
+    def last_kernel_ms(self) -> float:
+        return lib().artes_last_kernel_ms(self.h)
+
+    def close(self) -> None:
+        if getattr(self, "h", None) and self.h.value:
+            lib().artes_grid_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

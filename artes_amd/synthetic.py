@@ -1,0 +1,76 @@
+"""Synthetic atmospheres for the benchmark / parity configurations.
+
+All share: planet radius 1 R_J (``atmosphere.py:117``), a 100 km atmosphere with
+equally spaced radial faces, uniform extinction with radial optical depth ``tau``,
+single-scattering albedo ``omega`` (default 1), one wavelength (0.7 micron).
+The scattering matrices come from the restated opacity generators and the
+``simps`` renormalisation of ``atmosphere.py:60-65``, i.e. the reference's own
+setup path, not a hand-normalised table.
+
+=========  ==============================================  ==================
+config     scattering                                      grid (r x theta x phi)
+=========  ==============================================  ==================
+``iso``    isotropic                                       10 x 1 x 1
+``hg``     Henyey-Greenstein g=0.8, pLinear 0.5            32 x 1 x 1
+``ray3d``  Rayleigh, depolarisation 0                      32 x 16 x 32
+=========  ==============================================  ==================
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import opacity as op
+from .atmosphere import R_JUP
+
+CONFIGS = {
+    "iso": dict(kind="iso", nr=10, ntheta=1, nphi=1),
+    "hg": dict(kind="hg", nr=32, ntheta=1, nphi=1, g=0.8, p_linear=0.5),
+    "ray1d": dict(kind="ray", nr=32, ntheta=1, nphi=1),
+    "ray3d": dict(kind="ray", nr=32, ntheta=16, nphi=32),
+}
+
+
+def scatter_matrix(kind: str, wavelength=(0.7,), g: float = 0.8, p_linear: float = 0.5,
+                   depolarization: float = 0.0, normalizer: str = "simps") -> np.ndarray:
+    wl = list(wavelength)
+    if kind == "iso":
+        _, s = op.isotropic(wl)
+    elif kind == "hg":
+        _, s = op.henyey_greenstein(wl, g1=g, w1=1.0, p_linear=p_linear, p_circular=0.0)
+    elif kind == "ray":
+        _, s = op.rayleigh(wl, depolarization=depolarization)
+    else:
+        raise ValueError(f"unknown scattering kind {kind!r}")
+    return op.normalize_matrix(s, normalizer)
+
+
+def make(kind: str = "ray", nr: int = 32, ntheta: int = 16, nphi: int = 32, tau: float = 1.0,
+         omega: float = 1.0, height: float = 100e3, radius: float = R_JUP, wavelength=(0.7,),
+         g: float = 0.8, p_linear: float = 0.5, depolarization: float = 0.0,
+         share_matrix: bool = False, normalizer: str = "simps") -> dict:
+    """Return the nine atmosphere arrays (same keys/layout as ``read_atmosphere_fits``).
+
+    ``share_matrix=True`` returns the scatter matrix as a broadcast view (no 2880 x ncells
+    copy); the engine deduplicates per-cell matrices anyway, so this only saves host RAM.
+    """
+    nwav = len(wavelength)
+    radial = radius + np.linspace(0.0, height, nr + 1)
+    theta = np.linspace(0.0, 180.0, ntheta + 1)
+    phi = np.linspace(0.0, 360.0, nphi + 1)[:-1]
+    shape = (nphi, ntheta, nr)
+    kappa = tau / height
+    k_ext = np.full((nwav,) + shape, kappa)
+    k_sca = k_ext * omega
+    k_abs = k_ext - k_sca
+    sm = scatter_matrix(kind, wavelength, g=g, p_linear=p_linear, depolarization=depolarization, normalizer=normalizer)
+    full = np.broadcast_to(sm[:, :, :, None, None, None], (180, 16, nwav) + shape)
+    return dict(radial=radial, theta=theta, phi=phi, wavelength=np.asarray(wavelength, dtype=np.float64),
+                density=np.ones(shape), temperature=np.zeros(shape), scattering=k_sca, absorption=k_abs,
+                scattermatrix=full if share_matrix else np.ascontiguousarray(full))
+
+
+def make_config(name: str, **over) -> dict:
+    spec = dict(CONFIGS[name])
+    spec.update(over)
+    return make(**spec)

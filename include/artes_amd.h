@@ -1,0 +1,155 @@
+/*
+ * artes_amd.h -- C ABI of the MI355X photon-packet transport engine.
+ *
+ * This is the drop-in boundary for the reference's hot path: the OpenMP packet
+ * loop `radiative_transfer` (ARTES.f90:518-1006) together with the table set-up it
+ * consumes (`get_atmosphere` ARTES.f90:2054-2235, `grid_initialize(2)`
+ * ARTES.f90:2325-2357) and the per-thread detector reduction (ARTES.f90:957-975).
+ * In the reference these are module globals of one Fortran program; here they are
+ * a reentrant handle plus plain-pointer calls, so any host (ctypes, cgo, JNI, a
+ * Fortran `bind(C)` interface) can drive them.  See INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every array is C-order (row-major) double precision, laid out exactly as the
+ *     numpy view of the corresponding atmosphere.fits HDU: FITS axis 1 (the Fortran
+ *     first index) is the LAST C index.  E.g. the reference's
+ *     cell_scatter_matrix(r,theta,phi,lambda,16,180) (ARTES.f90:2196) is
+ *     scatter[180][16][nwav][nphi][ntheta][nr] here.
+ *   - Detector tensors are [4][4][ny][nx]: planes 0..2 are the reference's
+ *     detector(nx,ny,4,3) (ARTES.f90:84, 2543) in C order -- sum w, sum w^2 (per
+ *     peel), peel count -- for Stokes I,Q,U,V; plane 3 is an addition: the
+ *     packet-level second moment sum_p (X_p)^2 of each packet's contribution X_p to
+ *     the pixel, the honest Monte-Carlo variance (peels of one packet land in the
+ *     same pixel, so the per-peel sum w^2 underestimates it by ~1.7-3x).  Values
+ *     are in units of packet weight; the caller multiplies by package_energy
+ *     (ARTES.f90:964-970).
+ *   - totals[8]: sum_p T_p and sum_p T_p^2 of each packet's total detected weight
+ *     T_p per Stokes component (honest variance of the integrated photometry).
+ *   - Functions return 0 on success or a negative errno-style code; they never
+ *     exit the process (the reference calls exit(0) on fatal errors).
+ *   - Error-code counters: uint64_t err[ARTES_NUM_ERR], index = the reference's
+ *     "error NNN" number written to error.log (e.g. ARTES.f90:640, 3401).
+ */
+#ifndef ARTES_AMD_H
+#define ARTES_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ARTES_ABI_VERSION 1
+#define ARTES_NUM_ERR 64
+
+/* Counter slots (uint64_t counters[ARTES_NUM_COUNTERS]). */
+#define ARTES_CNT_CROSSINGS 0   /* cell_face calls (ARTES.f90:2800), all traces   */
+#define ARTES_CNT_SCATTERS  1   /* scatter_photon calls (ARTES.f90:1434)          */
+#define ARTES_CNT_PEELS     2   /* peel_photon calls (ARTES.f90:4710)             */
+#define ARTES_CNT_PACKETS   3   /* packets emitted                                 */
+#define ARTES_CNT_EXITED    4   /* packets that left the grid                      */
+#define ARTES_CNT_ABSORBED  5   /* surface absorption / roulette / minimum weight  */
+#define ARTES_CNT_DROPPED   6   /* cell_error or tau_first < 1e-6 drops            */
+#define ARTES_CNT_DETECTED  7   /* peels that reached the detector                 */
+#define ARTES_NUM_COUNTERS  8
+
+/* Raw atmosphere as read from atmosphere.fits (ARTES.f90:2067-2198). */
+typedef struct artes_grid_desc {
+    int32_t nr;              /* radial cells   (faces: nr+1)                       */
+    int32_t ntheta;          /* polar cells    (faces: ntheta+1)                   */
+    int32_t nphi;            /* azimuthal cells (faces: nphi, 2*pi implicit)       */
+    int32_t nwav;            /* wavelengths                                         */
+    const double* radial;    /* [nr+1]  m                                           */
+    const double* theta_deg; /* [ntheta+1] degrees                                  */
+    const double* phi_deg;   /* [nphi] degrees                                      */
+    const double* wavelength_um; /* [nwav] micron                                   */
+    const double* kappa_sca; /* [nwav][nphi][ntheta][nr]  m^-1                      */
+    const double* kappa_abs; /* [nwav][nphi][ntheta][nr]  m^-1                      */
+    const double* scatter;   /* [180][16][nwav][nphi][ntheta][nr]                   */
+    const double* temperature; /* [nphi][ntheta][nr] K, may be NULL (star source)   */
+    double oblateness;       /* planet:oblateness (ARTES.f90:469-471)               */
+} artes_grid_desc;
+
+/* Per-call run parameters: the globals radiative_transfer reads. */
+typedef struct artes_run_params {
+    int32_t wl_index;        /* 0-based wavelength (wl_count-1)                    */
+    int32_t nx, ny;          /* detector pixels (1x1 for spectrum/phase)           */
+    int32_t photon_source;   /* 1 = star (2 = planet: not yet supported -> -ENOSYS) */
+    int32_t photon_scattering; /* photon:scattering on/off                         */
+    int32_t phase_far;       /* phase_curve && det_phi >= 170 deg (ARTES.f90:1041) */
+    int32_t stellar_direction; /* star:direction (ARTES.f90:1080-1111)             */
+    int32_t cell_depth;      /* surface face index; <0 => computed (ARTES.f90:2329) */
+    double det_theta, det_phi; /* detector direction [rad], already clamped       */
+    double x_max, y_max;     /* image half-size [m] (ARTES.f90:475-479)            */
+    double fstop;            /* photon:fstop                                        */
+    double photon_minimum;   /* photon:minimum                                      */
+    double surface_albedo;   /* planet:surface_albedo                               */
+    double theta_star, phi_star; /* stellar direction [rad]                         */
+} artes_run_params;
+
+typedef struct artes_grid artes_grid;
+
+/* ABI / build identification. */
+int32_t artes_abi_version(void);
+const char* artes_build_info(void);
+
+/* Number of visible devices (hipGetDeviceCount); <0 on error. */
+int32_t artes_device_count(void);
+
+/* Build the device-resident tables for one atmosphere on `device`
+ * (replaces get_atmosphere post-processing + grid_initialize, ARTES.f90:2172-2270):
+ * extinction, albedo (floored at 1e-20), deduplicated scattering matrices with
+ * their cumulative sampling tables, p1j integrals and trig face tables. */
+int32_t artes_grid_create(const artes_grid_desc* desc, int32_t device, artes_grid** out);
+void    artes_grid_destroy(artes_grid* grid);
+
+/* cell_depth for a wavelength (grid_initialize(2), ARTES.f90:2329-2357). */
+int32_t artes_grid_cell_depth(const artes_grid* grid, int32_t wl_index);
+
+/* Number of distinct (cell, wavelength) scattering matrices kept after dedup. */
+int32_t artes_grid_num_matrices(const artes_grid* grid);
+
+/* Run packets [first_packet, first_packet + n_packets) of the global packet
+ * sequence keyed by `seed` (one xoroshiro128++ stream per global packet id, so
+ * results do not depend on how packets are sharded).  Synchronous; host outputs,
+ * all ACCUMULATED into (so shards/wavelengths can be summed in place):
+ *   detector   [4][4][ny][nx]   (see Conventions)
+ *   totals     [8]              (may be NULL)
+ *   counters   [ARTES_NUM_COUNTERS] (may be NULL)
+ *   err        [ARTES_NUM_ERR]  (may be NULL)
+ * Replaces radiative_transfer's packet loop + thread reduction (ARTES.f90:546-975). */
+int32_t artes_run(artes_grid* grid, const artes_run_params* params,
+                  uint64_t first_packet, uint64_t n_packets, uint64_t seed,
+                  double* detector, double* totals, uint64_t* counters, uint64_t* err);
+
+/* Asynchronous device variant: outputs are DEVICE pointers (e.g. torch tensors)
+ * that are accumulated into on `stream` (a hipStream_t, NULL = default stream);
+ * nothing is synchronised, so the caller can all-reduce `detector_dev` with RCCL
+ * on the same stream.  `kernel_ms` (may be NULL) receives nothing here; use
+ * artes_last_kernel_ms after synchronising. */
+int32_t artes_run_device(artes_grid* grid, const artes_run_params* params,
+                         uint64_t first_packet, uint64_t n_packets, uint64_t seed,
+                         double* detector_dev, double* totals_dev, uint64_t* counters_dev,
+                         uint64_t* err_dev, void* stream);
+
+/* Duration in ms of the transport kernel of the most recent run on this grid,
+ * measured with HIP events on the launch stream (valid once that stream has
+ * been synchronised). */
+double artes_last_kernel_ms(artes_grid* grid);
+
+/* Debug: per-packet records for packets [first, first+n) (n <= 2^24):
+ * rec[n][4] = { sum of peeled I weight, scatters, crossings, end state }.
+ * Used by the parity tests to compare trajectories with the CPU oracle. */
+int32_t artes_run_trace(artes_grid* grid, const artes_run_params* params,
+                        uint64_t first_packet, uint64_t n_packets, uint64_t seed,
+                        double* records);
+
+/* Last error message of the calling thread (static storage). */
+const char* artes_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ARTES_AMD_H */

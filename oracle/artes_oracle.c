@@ -1,0 +1,913 @@
+/*
+ * artes_oracle.c -- CPU ORACLE (test infrastructure only).
+ *
+ * A line-by-line C restatement of the reference's photon-packet loop
+ * `radiative_transfer` (src/ARTES.f90:518-1006) and its callees, used ONLY by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.
+ * The product path (artes_amd/, libartes_hip.so) never links or calls this file.
+ *
+ * Parity pinning: the reference has no tests or golden vectors and
+ * cannot be rebuilt under this pipeline's rules (it needs cfitsio, which ships in
+ * the reference only as a prebuilt binary, plus a stand-in for the GNU STAT
+ * intrinsic).  This restatement is pinned (tests/test_oracle.py) against
+ *   (a) analytic known-answer tests (single-scattering limit, energy normalisation,
+ *       isotropic Q=U=V=0, Rayleigh polarisation at 90 degrees), and
+ *   (b) frozen reference outputs produced when the survey ran the reference
+ *       (tests/golden/, provenance in tests/golden/README.md),
+ * statistically, within the Monte-Carlo sigma the reference itself reports.
+ *
+ * Deliberate differences from the Fortran, all documented in DESIGN.md:
+ *   - RNG: the reference's clock-seeded Marsaglia-Zaman generator per OpenMP thread
+ *     (ARTES.f90:4175-4230) is replaced by one xoroshiro128++ stream per global
+ *     packet id (seeded from the splitmix64 sequence of mix(seed) + 2*id*gamma), shared with the GPU engine, so
+ *     runs are reproducible and shard-count independent.
+ *   - gamma = albedo/(1-fstop) is per packet (the reference shares it between
+ *     threads, a data race, ARTES.f90:541, 804).
+ *   - A packet whose cell_face reports cell_error is dropped immediately; the
+ *     reference keeps stepping with undefined cell indices before dropping it.
+ *   - error.log lines become counters err[NNN].
+ * Only the star source (photon:source=star) is restated; see DESIGN.md §8f.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/artes_amd.h"
+
+#define PI_ (4.0 * atan(1.0))
+
+/* ----------------------------------------------------------------- RNG ---- */
+typedef struct { uint64_t s0, s1; } rng_t;
+
+static inline uint64_t splitmix64(uint64_t* x) {
+    uint64_t z = (*x += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+static inline uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+/* stream of packet `id`: the splitmix64 sequence started at mix(seed) + 2*id*gamma, so
+ * every (seed, id) pair gets its own non-overlapping pair of splitmix64 outputs */
+static inline void rng_seed(rng_t* r, uint64_t seed, uint64_t id) {
+    uint64_t k = seed;
+    uint64_t sm = splitmix64(&k) + 2ULL * id * 0x9e3779b97f4a7c15ULL;
+    r->s0 = splitmix64(&sm);
+    r->s1 = splitmix64(&sm);
+    if ((r->s0 | r->s1) == 0) r->s1 = 1;
+}
+/* xi in (0,1): the reference's random() returns an open-interval double (ARTES.f90:4216-4228) */
+static inline double rng_uniform(rng_t* r) {
+    const uint64_t s0 = r->s0;
+    uint64_t s1 = r->s1;
+    const uint64_t res = rotl64(s0 + s1, 17) + s0;
+    s1 ^= s0;
+    r->s0 = rotl64(s0, 49) ^ s1 ^ (s1 << 21);
+    r->s1 = rotl64(s1, 28);
+    return ((double)(res >> 11) + 0.5) * 0x1.0p-53;
+}
+
+/* ----------------------------------------------------------------- grid --- */
+typedef struct oracle_grid {
+    int nr, ntheta, nphi, nwav, ncell;
+    double *rfront, *thetafront, *theta_grid_cos, *theta_grid_tan, *phifront, *phi_grid_sin, *phi_grid_cos;
+    int* thetaplane;
+    double* cell_opacity;   /* [nwav][ncell] */
+    double* cell_albedo;    /* [nwav][ncell] */
+    double* p1j_int;        /* [nwav][ncell][4] */
+    const double* scatter;  /* raw [180][16][nwav][ncell] */
+    double oblate_x, oblate_y, oblate_z;
+    double sinbeta[361], cosbeta[361], sin2beta[361], cos2beta[361]; /* 1-based as in Fortran */
+} oracle_grid;
+
+typedef struct ctx {
+    const oracle_grid* g;
+    const artes_run_params* p;
+    int wl, cell_depth, nx, ny;
+    double det[3], sin_det_theta, cos_det_theta, sin_det_phi, cos_det_phi;
+    uint64_t* err;         /* thread-private [ARTES_NUM_ERR] */
+    uint64_t* cnt;         /* thread-private [ARTES_NUM_COUNTERS] */
+    double* detector;      /* thread-private [4][4][ny][nx] */
+    double* totals;        /* thread-private [8] */
+    double peel_sum;       /* per-packet trace record */
+    int cur_pix;           /* pixel of the packet's running contribution (-1: none) */
+    double cur_sum[4];     /* running contribution of this packet to cur_pix */
+    double pkt_tot[4];     /* this packet's total detected weight */
+} ctx;
+
+static inline int cidx(const oracle_grid* g, const int c[3]) { return (c[2] * g->ntheta + c[1]) * g->nr + c[0]; }
+static inline double kappa(const ctx* X, const int c[3]) { return X->g->cell_opacity[(size_t)X->wl * X->g->ncell + cidx(X->g, c)]; }
+/* cell_scatter_matrix(cell, wl, elem(1..16), angle(1..180)) -- ARTES.f90:2196 */
+static inline double smat(const ctx* X, const int c[3], int elem1, int ang1) {
+    const oracle_grid* g = X->g;
+    return g->scatter[(((size_t)(ang1 - 1) * 16 + (elem1 - 1)) * g->nwav + X->wl) * g->ncell + cidx(g, c)];
+}
+static inline void error_log(ctx* X, int code) { if (code >= 0 && code < ARTES_NUM_ERR) X->err[code]++; }
+
+oracle_grid* oracle_grid_create(const artes_grid_desc* d) {
+    oracle_grid* g = (oracle_grid*)calloc(1, sizeof(oracle_grid));
+    if (!g) return NULL;
+    const double pi = PI_;
+    g->nr = d->nr; g->ntheta = d->ntheta; g->nphi = d->nphi; g->nwav = d->nwav;
+    g->ncell = d->nr * d->ntheta * d->nphi;
+    g->rfront = (double*)malloc(sizeof(double) * (g->nr + 1));
+    g->thetafront = (double*)malloc(sizeof(double) * (g->ntheta + 1));
+    g->theta_grid_cos = (double*)malloc(sizeof(double) * (g->ntheta + 1));
+    g->theta_grid_tan = (double*)malloc(sizeof(double) * (g->ntheta + 1));
+    g->thetaplane = (int*)malloc(sizeof(int) * (g->ntheta + 1));
+    g->phifront = (double*)malloc(sizeof(double) * g->nphi);
+    g->phi_grid_sin = (double*)malloc(sizeof(double) * g->nphi);
+    g->phi_grid_cos = (double*)malloc(sizeof(double) * g->nphi);
+    for (int i = 0; i <= g->nr; i++) g->rfront[i] = d->radial[i];
+    for (int i = 0; i <= g->ntheta; i++) {           /* ARTES.f90:2097-2106 */
+        double t = d->theta_deg[i];
+        g->thetaplane[i] = (t < 90.0 - 1.e-6 || t > 90.0 + 1.e-6) ? 1 : 2;
+        g->thetafront[i] = t * pi / 180.0;
+        g->theta_grid_cos[i] = cos(g->thetafront[i]);   /* ARTES.f90:2261-2264 */
+        g->theta_grid_tan[i] = tan(g->thetafront[i]);
+    }
+    for (int i = 0; i < g->nphi; i++) {
+        g->phifront[i] = d->phi_deg[i] * pi / 180.0;
+        g->phi_grid_cos[i] = cos(g->phifront[i]);       /* ARTES.f90:2267-2270 */
+        g->phi_grid_sin[i] = sin(g->phifront[i]);
+    }
+    /* beta tables, 1-based (ARTES.f90:404-420) */
+    for (int i = 1; i <= 180; i++) {
+        g->cosbeta[i] = (cos((double)i * pi / 180.0) + cos((double)(i - 1) * pi / 180.0)) / 2.0;
+        g->cosbeta[i + 180] = -g->cosbeta[i];
+        g->sinbeta[i] = (sin((double)i * pi / 180.0) + sin((double)(i - 1) * pi / 180.0)) / 2.0;
+        g->sinbeta[i + 180] = -g->sinbeta[i];
+        g->cos2beta[i] = (cos(2.0 * (double)i * pi / 180.0) + cos(2.0 * (double)(i - 1) * pi / 180.0)) / 2.0;
+        g->cos2beta[i + 180] = g->cos2beta[i];
+        g->sin2beta[i] = (sin(2.0 * (double)i * pi / 180.0) + sin(2.0 * (double)(i - 1) * pi / 180.0)) / 2.0;
+        g->sin2beta[i + 180] = g->sin2beta[i];
+    }
+    size_t n = (size_t)g->nwav * g->ncell;
+    g->cell_opacity = (double*)malloc(sizeof(double) * n);
+    g->cell_albedo = (double*)malloc(sizeof(double) * n);
+    g->p1j_int = (double*)calloc(n * 4, sizeof(double));
+    for (size_t i = 0; i < n; i++) {                      /* ARTES.f90:2178-2188 */
+        double ext = d->kappa_sca[i] + d->kappa_abs[i];
+        double alb = 0.0;
+        g->cell_opacity[i] = ext;
+        if (ext > 0.0) alb = d->kappa_sca[i] / ext;
+        if (alb < 1.e-20) alb = 1.e-20;
+        g->cell_albedo[i] = alb;
+    }
+    g->scatter = d->scatter;
+    for (int m = 0; m < g->nwav; m++)                      /* ARTES.f90:2215-2230 */
+        for (int n1 = 1; n1 <= 180; n1++)
+            for (int j = 0; j < 4; j++) {
+                const double* src = d->scatter + (((size_t)(n1 - 1) * 16 + j) * g->nwav + m) * g->ncell;
+                double* dst = g->p1j_int + (size_t)m * g->ncell * 4;
+                for (int c = 0; c < g->ncell; c++) dst[c * 4 + j] += src[c] * g->sinbeta[n1] * pi / 180.0;
+            }
+    g->oblate_x = 1.0 / (1.0 - d->oblateness);                 /* ARTES.f90:469-471 */
+    g->oblate_y = g->oblate_x;
+    g->oblate_z = 1.0;
+    return g;
+}
+
+void oracle_grid_destroy(oracle_grid* g) {
+    if (!g) return;
+    free(g->rfront); free(g->thetafront); free(g->theta_grid_cos); free(g->theta_grid_tan);
+    free(g->thetaplane); free(g->phifront); free(g->phi_grid_sin); free(g->phi_grid_cos);
+    free(g->cell_opacity); free(g->cell_albedo); free(g->p1j_int);
+    free(g);
+}
+
+/* grid_initialize(2), star branch (ARTES.f90:2329-2357) */
+int oracle_cell_depth(const oracle_grid* g, int wl) {
+    int cell_max = 1000000, cell_depth = 0;
+    for (int j = 0; j < g->ntheta; j++)
+        for (int k = 0; k < g->nphi; k++) {
+            double tot = 0.0;
+            for (int i = 0; i < g->nr; i++) {
+                int c[3] = {g->nr - i - 1, j, k};
+                tot += g->cell_opacity[(size_t)wl * g->ncell + cidx(g, c)] * (g->rfront[g->nr - i] - g->rfront[g->nr - i - 1]);
+                cell_depth = g->nr - i - 1;
+                if (tot > 30.0) break;
+            }
+            if (cell_depth < cell_max) cell_max = cell_depth;
+        }
+    return cell_max;
+}
+
+/* ------------------------------------------------------- geometry -------- */
+/* quadratic_equation (ARTES.f90:4154-4173) */
+static inline void quadratic_equation(double a, double b, double c, double s[2]) {
+    s[0] = 0.0; s[1] = 0.0;
+    double disc = b * b - 4.0 * a * c;
+    if (disc >= 0.0) {
+        double q = -0.5 * (b + copysign(1.0, b) * sqrt(disc));
+        if (fabs(a) > 1.e-100) s[0] = q / a;
+        if (fabs(q) > 1.e-100) s[1] = c / q;
+    }
+}
+
+/* the repeated root-selection block of cell_face, e.g. ARTES.f90:2897-2907 */
+static inline double pick_root(const double s[2], double tol) {
+    if (s[0] > tol && s[1] <= tol && s[0] < 1.e100) return s[0];
+    if (s[1] > tol && s[0] <= tol && s[1] < 1.e100) return s[1];
+    if (s[0] > tol && s[1] > tol) {
+        if (s[0] < 1.e100 && s[0] < s[1]) return s[0];
+        if (s[1] < 1.e100 && s[1] < s[0]) return s[1];
+    }
+    return 0.0;
+}
+
+/* next_cell (ARTES.f90:2671-2798) */
+static void next_cell(ctx* X, const int cf[2], const int nf[2], const int cin[3], int cout[3]) {
+    const oracle_grid* g = X->g;
+    const double pi = PI_;
+    cout[0] = cout[1] = cout[2] = 0;
+    if (nf[0] == 1) {
+        if (cf[0] == 1 && nf[1] == cf[1]) { cout[0] = cin[0] + 1; cout[1] = cin[1]; cout[2] = cin[2]; }
+        else if (nf[1] == cin[0]) { cout[0] = cin[0] - 1; cout[1] = cin[1]; cout[2] = cin[2]; }
+        else if (nf[1] == cin[0] + 1) { cout[0] = cin[0] + 1; cout[1] = cin[1]; cout[2] = cin[2]; }
+        else error_log(X, 22);
+    }
+    if (nf[0] == 2) {
+        if (cf[0] == 2 && nf[1] == cf[1] && g->thetafront[nf[1]] < pi / 2.0) { cout[0] = cin[0]; cout[1] = cin[1] + 1; cout[2] = cin[2]; }
+        else if (cf[0] == 2 && nf[1] == cf[1] && g->thetafront[nf[1]] > pi / 2.0) { cout[0] = cin[0]; cout[1] = cin[1] - 1; cout[2] = cin[2]; }
+        else if (nf[1] == cin[1]) { cout[0] = cin[0]; cout[1] = cin[1] - 1; cout[2] = cin[2]; }
+        else if (nf[1] == cin[1] + 1) { cout[0] = cin[0]; cout[1] = cin[1] + 1; cout[2] = cin[2]; }
+        else error_log(X, 23);
+    }
+    if (nf[0] == 3) {
+        if (cin[2] == g->nphi - 1 && nf[1] == 0) { cout[0] = cin[0]; cout[1] = cin[1]; cout[2] = 0; }
+        else if (cin[2] == 0 && nf[1] == 0) { cout[0] = cin[0]; cout[1] = cin[1]; cout[2] = g->nphi - 1; }
+        else if (nf[1] == cin[2] + 1) { cout[0] = cin[0]; cout[1] = cin[1]; cout[2] = cin[2] + 1; }
+        else if (nf[1] == cin[2]) { cout[0] = cin[0]; cout[1] = cin[1]; cout[2] = cin[2] - 1; }
+        else error_log(X, 24);
+    }
+}
+
+/* theta-cone candidate with the nappe filter (e.g. ARTES.f90:3026-3064) */
+static double cone_distance(const oracle_grid* g, int face, double x, double y, double z, const double n[3],
+                            double a, double b, double c, double tol) {
+    const double pi = PI_;
+    double tt = g->theta_grid_tan[face];
+    double qa = a * a * n[0] * n[0] + b * b * n[1] * n[1] - c * c * n[2] * n[2] * tt * tt;
+    double qb = 2.0 * (a * a * x * n[0] + b * b * y * n[1] - c * c * z * n[2] * tt * tt);
+    double qc = a * a * x * x + b * b * y * y - c * c * z * z * tt * tt;
+    double s[2];
+    quadratic_equation(qa, qb, qc, s);
+    for (int k = 0; k < 2; k++) {
+        if (s[k] > 1.e-15) {
+            double zt = z + s[k] * n[2];
+            if ((zt > 0.0 && g->thetafront[face] > pi / 2.0) || (zt < 0.0 && g->thetafront[face] < pi / 2.0)) s[k] = 0.0;
+        }
+    }
+    return pick_root(s, tol);
+}
+
+static double sphere_distance(const oracle_grid* g, int face, double x, double y, double z, const double n[3],
+                              double a, double b, double c, double tol) {
+    double qa = a * a * n[0] * n[0] + b * b * n[1] * n[1] + c * c * n[2] * n[2];
+    double qb = 2.0 * (a * a * x * n[0] + b * b * y * n[1] + c * c * z * n[2]);
+    double qc = a * a * x * x + b * b * y * y + c * c * z * z - g->rfront[face] * g->rfront[face];
+    double s[2];
+    quadratic_equation(qa, qb, qc, s);
+    return pick_root(s, tol);
+}
+
+/* cell_face (ARTES.f90:2800-3470) */
+static void cell_face(ctx* X, double x, double y, double z, const double n[3], const int cf[2], int nf[2],
+                      double* face_distance, int* grid_exit, const int cell[3], int cout[3], int* cell_error) {
+    const oracle_grid* g = X->g;
+    const double pi = PI_;
+    int face[3][3];
+    double distance[3][3];
+    double sp[2] = {0.0, 0.0};
+    X->cnt[ARTES_CNT_CROSSINGS]++;
+    if (cell[0] < X->cell_depth) error_log(X, 25);
+    *grid_exit = 0;
+    *cell_error = 0;
+    memset(distance, 0, sizeof(distance));
+    int floc0 = 0, floc1 = 0;
+    const double a = 1.0 / g->oblate_x, b = 1.0 / g->oblate_y, c = 1.0 / g->oblate_z;
+
+    face[0][0] = cell[0]; face[0][1] = cell[0] + 1; face[0][2] = -999;
+    face[1][0] = cell[1]; face[1][1] = cell[1] + 1; face[1][2] = -999;
+    face[2][0] = cell[2]; face[2][1] = cell[2] + 1; face[2][2] = -999;
+    if (face[2][1] == g->nphi) face[2][1] = 0;
+
+    if (cf[0] == 1) {
+        face[0][0] = cf[1] - 1; face[0][1] = cf[1] + 1; face[0][2] = cf[1];
+    } else if (cf[0] == 2) {
+        face[1][0] = cf[1] - 1; face[1][1] = cf[1] + 1; face[1][2] = cf[1];
+    } else if (cf[0] == 3) {
+        face[2][0] = (cf[1] == 0) ? g->nphi - 1 : cf[1] - 1;
+        face[2][1] = (cf[1] == g->nphi - 1) ? 0 : cf[1] + 1;
+    }
+
+    /* radial faces (ARTES.f90:2885-3010) */
+    if (cf[0] == 1) {
+        if (cell[0] == cf[1] - 1) distance[0][0] = sphere_distance(g, face[0][0], x, y, z, n, a, b, c, 1.e-15);
+        else if (cell[0] == cf[1]) distance[0][1] = sphere_distance(g, face[0][1], x, y, z, n, a, b, c, 1.e-15);
+        if (cell[0] == cf[1] - 1) distance[0][2] = sphere_distance(g, face[0][2], x, y, z, n, a, b, c, 1.e-3);
+        else if (cell[0] == cf[1]) { }
+        else error_log(X, 27);
+    } else {
+        distance[0][0] = sphere_distance(g, face[0][0], x, y, z, n, a, b, c, 1.e-15);
+        distance[0][1] = sphere_distance(g, face[0][1], x, y, z, n, a, b, c, 1.e-15);
+    }
+
+    /* theta faces (ARTES.f90:3014-3290) */
+    if (cf[0] == 2 && face[1][2] == -999) error_log(X, 28);
+    if (cf[0] == 2) {
+        if (cell[1] == cf[1] - 1 && face[1][0] != 0) {
+            if (g->thetaplane[face[1][0]] == 1) distance[1][0] = cone_distance(g, face[1][0], x, y, z, n, a, b, c, 1.e-15);
+            else if (g->thetaplane[face[1][0]] == 2) { if (-z / n[2] > 0.0 && n[2] > 1.e-15) distance[1][0] = -z / n[2]; }
+        } else if (cell[1] == cf[1] && face[1][1] != g->ntheta) {
+            if (g->thetaplane[face[1][1]] == 1) distance[1][1] = cone_distance(g, face[1][1], x, y, z, n, a, b, c, 1.e-15);
+            else if (g->thetaplane[face[1][1]] == 2) { if (-z / n[2] > 0.0 && n[2] < -1.e-15) distance[1][1] = -z / n[2]; }
+        }
+        if ((g->thetafront[face[1][2]] < pi / 2.0 && cell[1] == cf[1] - 1) ||
+            (g->thetafront[face[1][2]] > pi / 2.0 && cell[1] == cf[1])) {
+            if (g->thetaplane[face[1][2]] == 1) distance[1][2] = cone_distance(g, face[1][2], x, y, z, n, a, b, c, 1.e-3);
+        }
+    } else {
+        if (face[1][0] < 0 || face[1][0] > g->ntheta) { error_log(X, 29); face[1][0] = 0; }
+        if (face[1][0] != 0) {
+            if (g->thetaplane[face[1][0]] == 1) distance[1][0] = cone_distance(g, face[1][0], x, y, z, n, a, b, c, 1.e-15);
+            else if (g->thetaplane[face[1][0]] == 2) { if (-z / n[2] > 0.0 && n[2] > 1.e-15) distance[1][0] = -z / n[2]; }
+        }
+        if (face[1][1] != g->ntheta) {
+            if (g->thetaplane[face[1][1]] == 1) distance[1][1] = cone_distance(g, face[1][1], x, y, z, n, a, b, c, 1.e-15);
+            else if (g->thetaplane[face[1][1]] == 2) { if (-z / n[2] > 0.0 && n[2] < -1.e-15) distance[1][1] = -z / n[2]; }
+        }
+    }
+
+    /* phi faces (ARTES.f90:3292-3350) */
+    if (cf[0] == 3) {
+        if (cell[2] == cf[1] - 1 || (cell[2] == g->nphi - 1 && cf[1] == 0)) {
+            double den = b * n[1] * g->phi_grid_cos[face[2][0]] - a * n[0] * g->phi_grid_sin[face[2][0]];
+            if (fabs(den) > 0.0) {
+                sp[0] = (a * x * g->phi_grid_sin[face[2][0]] - b * y * g->phi_grid_cos[face[2][0]]) / den;
+                if (sp[0] > 1.e-15 && sp[0] < 1.e100) distance[2][0] = sp[0];
+            }
+        } else if (cell[2] == cf[1]) {
+            double den = b * n[1] * g->phi_grid_cos[face[2][1]] - a * n[0] * g->phi_grid_sin[face[2][1]];
+            if (fabs(den) > 0.0) {
+                sp[1] = (a * x * g->phi_grid_sin[face[2][1]] - b * y * g->phi_grid_cos[face[2][1]]) / den;
+                if (sp[1] > 1.e-15 && sp[0] < 1.e100) distance[2][1] = sp[1];   /* sic: tests sp[0] (ARTES.f90:3318) */
+            }
+        }
+    } else if (g->nphi > 1) {
+        double den = b * n[1] * g->phi_grid_cos[face[2][0]] - a * n[0] * g->phi_grid_sin[face[2][0]];
+        if (fabs(den) > 0.0) {
+            sp[0] = (a * x * g->phi_grid_sin[face[2][0]] - b * y * g->phi_grid_cos[face[2][0]]) / den;
+            if (sp[0] > 1.e-15 && sp[0] < 1.e100) distance[2][0] = sp[0];
+        }
+        if (fabs(n[1] * g->phi_grid_cos[face[2][1]] - n[0] * g->phi_grid_sin[face[2][1]]) > 0.0) {   /* sic: no a, b (ARTES.f90:3341) */
+            sp[1] = (a * x * g->phi_grid_sin[face[2][1]] - b * y * g->phi_grid_cos[face[2][1]]) /
+                    (b * n[1] * g->phi_grid_cos[face[2][1]] - a * n[0] * g->phi_grid_sin[face[2][1]]);
+            if (sp[1] > 1.e-15 && sp[0] < 1.e100) distance[2][1] = sp[1];
+        }
+    }
+
+    /* nearest face: 'large' (>1e-9) then 'small' (>1e-12) solutions, j-major scan (ARTES.f90:3358-3418) */
+    *face_distance = 1.e100;
+    for (int j = 0; j < 3; j++)
+        for (int i = 0; i < 3; i++)
+            if (distance[i][j] > 1.e-9 && distance[i][j] < *face_distance) { *face_distance = distance[i][j]; floc0 = i + 1; floc1 = j + 1; }
+    if (floc0 == 0) {
+        *face_distance = 1.e100;
+        for (int j = 0; j < 3; j++)
+            for (int i = 0; i < 3; i++)
+                if (distance[i][j] > 1.e-12 && distance[i][j] < *face_distance) { *face_distance = distance[i][j]; floc0 = i + 1; floc1 = j + 1; }
+        if (floc0 == 0) { error_log(X, 31); *cell_error = 1; }
+    }
+
+    nf[0] = floc0;
+    nf[1] = (floc0 == 0) ? -999 : face[floc0 - 1][floc1 - 1];
+    if (nf[1] == -999) {
+        error_log(X, 33);
+        *cell_error = 1;
+        cout[0] = cell[0]; cout[1] = cell[1]; cout[2] = cell[2];
+    } else {
+        next_cell(X, cf, nf, cell, cout);
+    }
+    if (nf[0] == 1 && nf[1] == g->nr) *grid_exit = 1;
+    if (cf[0] == 1 && cf[1] == X->cell_depth && nf[0] == 1 && nf[1] == X->cell_depth) { error_log(X, 34); *cell_error = 1; }
+    else if (cout[0] == g->nr && !*grid_exit) { error_log(X, 35); *cell_error = 1; }
+    else if (cout[1] == g->ntheta) { error_log(X, 36); *cell_error = 1; }
+    else if (cell[0] == cout[0] && cell[1] == cout[1] && cell[2] == cout[2] && !*grid_exit) { error_log(X, 37); *cell_error = 1; }
+}
+
+/* ------------------------------------------------------ scattering ------- */
+/* mueller_matrix_filler (ARTES.f90:1934-1960), m = {m11, m12, m21, m22} */
+static void mueller_matrix_filler(double psi, double m[4]) {
+    const double pi = PI_;
+    double c2p = cos(2.0 * psi);
+    double s2p = sqrt(1.0 - c2p * c2p);
+    if (psi > pi / 2.0 && psi < pi) s2p = -s2p;
+    else if (psi > 3.0 * pi / 2.0 && psi < 2.0 * pi) s2p = -s2p;
+    else if (psi > -pi / 2.0 && psi < 0.0) s2p = -s2p;
+    else if (psi > -2.0 * pi && psi < -3.0 * pi / 2.0) s2p = -s2p;
+    m[0] = c2p; m[2] = -s2p; m[1] = s2p; m[3] = c2p;
+}
+
+/* polarization_rotation (ARTES.f90:1663-1932); sc is scatter(4,4) row-major */
+static void polarization_rotation(ctx* X, double alpha, double beta, const double sin_[4], const double sc[16],
+                                  const double dir[3], const double dnew[3], double sout[4], int peeling) {
+    const double pi = PI_;
+    double beta2 = 0.0, m[4], rot[4], ssc[4], norm;
+    if (fabs(alpha) < 1.0 && fabs(dnew[2]) < 1.0) {
+        double num = (dir[2] - dnew[2] * alpha) / (sqrt(1.0 - alpha * alpha) * sqrt(1.0 - dnew[2] * dnew[2]));
+        if (fabs(num) <= 1.0) beta2 = acos(num);
+        else if (num > 1.0 && num < 1.00001) beta2 = 0.0;
+        else if (num < -1.0 && num > -1.00001) beta2 = pi;
+        else error_log(X, 11);
+        mueller_matrix_filler(beta, m);
+        rot[0] = sin_[0];
+        rot[1] = m[0] * sin_[1] + m[1] * sin_[2];
+        rot[2] = m[2] * sin_[1] + m[3] * sin_[2];
+        rot[3] = sin_[3];
+        double pr = sqrt(rot[1] * rot[1] + rot[2] * rot[2] + rot[3] * rot[3]);
+        if (pr > 0.0) norm = sqrt(sin_[1] * sin_[1] + sin_[2] * sin_[2] + sin_[3] * sin_[3]) / pr;
+        else norm = 1.0;
+        if (norm < 1.0 || norm > 1.0) { rot[1] *= norm; rot[2] *= norm; rot[3] *= norm; }
+        for (int i = 0; i < 4; i++) ssc[i] = sc[i * 4 + 0] * rot[0] + sc[i * 4 + 1] * rot[1] + sc[i * 4 + 2] * rot[2] + sc[i * 4 + 3] * rot[3];
+        if (!peeling) {
+            if (ssc[0] > 0.0) { norm = rot[0] / ssc[0]; for (int i = 0; i < 4; i++) ssc[i] *= norm; }
+            else error_log(X, 12);
+        }
+        if (beta >= 0.0 && beta < pi) mueller_matrix_filler(beta2, m);
+        else if (beta >= pi && beta < 2.0 * pi) mueller_matrix_filler(-beta2, m);
+        sout[0] = ssc[0];
+        sout[1] = m[0] * ssc[1] + m[1] * ssc[2];
+        sout[2] = m[2] * ssc[1] + m[3] * ssc[2];
+        sout[3] = ssc[3];
+        double po = sqrt(sout[1] * sout[1] + sout[2] * sout[2] + sout[3] * sout[3]);
+        if (po > 0.0) norm = sqrt(ssc[1] * ssc[1] + ssc[2] * ssc[2] + ssc[3] * ssc[3]) / po;
+        else norm = 1.0;
+        if (norm < 1.0 || norm > 1.0) { sout[1] *= norm; sout[2] *= norm; sout[3] *= norm; }
+    } else if (alpha >= 1.0 && alpha < 1.0001) {
+        for (int i = 0; i < 4; i++) sout[i] = sin_[i];
+        error_log(X, 13);
+    } else if (alpha <= -1.0 && alpha > -1.0001) {
+        for (int i = 0; i < 4; i++) ssc[i] = sc[i * 4 + 0] * sin_[0] + sc[i * 4 + 1] * sin_[1] + sc[i * 4 + 2] * sin_[2] + sc[i * 4 + 3] * sin_[3];
+        if (peeling) for (int i = 0; i < 4; i++) sout[i] = ssc[i];
+        else if (ssc[0] > 0.0) { norm = sin_[0] / ssc[0]; for (int i = 0; i < 4; i++) sout[i] = norm * ssc[i]; }
+        else { for (int i = 0; i < 4; i++) sout[i] = 0.0; error_log(X, 14); }
+        error_log(X, 15);
+    } else {
+        error_log(X, 16);
+    }
+}
+
+/* direction_cosine (ARTES.f90:1962-2052) */
+static void direction_cosine(ctx* X, double alpha, double beta, const double dir[3], double dnew[3]) {
+    const double pi = PI_;
+    double cto = dir[2] / sqrt(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+    double sto = sqrt(1.0 - cto * cto);
+    double phi_old = atan2(dir[1], dir[0]);
+    if (phi_old < 0.0) phi_old += 2.0 * pi;
+    double ctn = 0.0, phi_new = 0.0, spn = 0.0;
+    if (beta >= pi && beta < 2.0 * pi) ctn = cto * alpha + sto * sqrt(1.0 - alpha * alpha) * cos(2.0 * pi - beta);
+    else if (beta >= 0.0 && beta < pi) ctn = cto * alpha + sto * sqrt(1.0 - alpha * alpha) * cos(beta);
+    else error_log(X, 18);
+    double stn = sqrt(1.0 - ctn * ctn);
+    double num = (alpha - ctn * cto) / (stn * sto);
+    if (num >= 1.0) num = 1.0 - 1.e-10;
+    else if (num <= -1.0) num = -1.0 + 1.e-10;
+    if (fabs(num) <= 1.0) {
+        if (beta >= pi && beta < 2.0 * pi) phi_new = phi_old - acos(num);
+        else if (beta >= 0.0 && beta < pi) phi_new = phi_old + acos(num);
+        else error_log(X, 19);
+    } else {
+        error_log(X, 20);
+    }
+    if (phi_new < 0.0) phi_new += 2.0 * pi;
+    if (phi_new > 2.0 * pi) phi_new -= 2.0 * pi;
+    double cpn = cos(phi_new);
+    if (phi_new >= 0.0 && phi_new < pi) spn = sqrt(1.0 - cpn * cpn);
+    else if (phi_new >= pi && phi_new <= 2.0 * pi) spn = -sqrt(1.0 - cpn * cpn);
+    else error_log(X, 21);
+    dnew[0] = stn * cpn;
+    dnew[1] = stn * spn;
+    dnew[2] = ctn;
+}
+
+/* scattering_angle_sampling (ARTES.f90:1534-1661): linear CDF scans, as the reference */
+static void scattering_angle_sampling(ctx* X, rng_t* rng, const double st[4], double* alpha, double* beta, const int cell[3]) {
+    const oracle_grid* g = X->g;
+    const double pi = PI_;
+    double inten, cum[181], xi, s;
+    const double* p1j = g->p1j_int + ((size_t)X->wl * g->ncell + cidx(g, cell)) * 4;
+    cum[0] = 0.0;
+    for (int i = 1; i <= 180; i++) {
+        inten = p1j[0] * st[0] + p1j[1] * st[1] * g->cos2beta[i] + p1j[1] * st[2] * g->sin2beta[i] -
+                p1j[2] * st[1] * g->sin2beta[i] + p1j[2] * st[2] * g->cos2beta[i] + p1j[3] * st[3];
+        cum[i] = cum[i - 1] + inten;
+    }
+    xi = rng_uniform(rng);
+    s = xi * cum[180];
+    *beta = 0.0;
+    for (int i = 1; i <= 180; i++) {
+        if (s >= cum[i - 1] && s <= cum[i]) {
+            *beta = ((double)i - (double)(i - 1)) * (s - cum[i - 1]) / (cum[i] - cum[i - 1]) + (double)(i - 1);
+            *beta = *beta * pi / 180.0;
+            break;
+        }
+        if (i == 180) error_log(X, 6);
+    }
+    xi = rng_uniform(rng);
+    if (xi > 0.5) *beta = *beta + pi;
+    if (*beta >= 2.0 * pi) *beta = 2.0 * pi - 1.e-10;
+    if (*beta <= 0.0) *beta = -2.0 * pi + 1.e-10;
+
+    double c2b = cos(2.0 * *beta);
+    double s2b = sqrt(1.0 - c2b * c2b);
+    if (*beta > pi / 2.0 && *beta < pi) s2b = -s2b;
+    else if (*beta > 3.0 * pi / 2.0 && *beta < 2.0 * pi) s2b = -s2b;
+    else if (*beta > -pi / 2.0 && *beta < 0.0) s2b = -s2b;
+    else if (*beta > -2.0 * pi && *beta < -3.0 * pi / 2.0) s2b = -s2b;
+
+    for (int i = 1; i <= 180; i++) {
+        inten = smat(X, cell, 1, i) * st[0] + smat(X, cell, 2, i) * c2b * st[1] + smat(X, cell, 2, i) * s2b * st[2] -
+                smat(X, cell, 3, i) * s2b * st[1] + smat(X, cell, 3, i) * c2b * st[2] + smat(X, cell, 4, i) * st[3];
+        inten = inten * g->sinbeta[i] * pi / 180.0;
+        cum[i] = cum[i - 1] + inten;
+    }
+    xi = rng_uniform(rng);
+    s = xi * cum[180];
+    *alpha = 0.0;
+    for (int i = 1; i <= 180; i++) {
+        if (s >= cum[i - 1] && s <= cum[i]) {
+            double a = ((double)i - (double)(i - 1)) * (s - cum[i - 1]) / (cum[i] - cum[i - 1]) + (double)(i - 1);
+            *alpha = cos(a * pi / 180.0);
+            if (fabs(*alpha) >= 1.0) error_log(X, 56);
+            break;
+        }
+    }
+    if (*alpha >= 1.0) *alpha = 1.0 - 1.e-10;
+    if (*alpha <= -1.0) *alpha = -1.0 + 1.e-10;
+}
+
+/* matrix interpolation at angle acos(mu) [rad] between bin centres (ARTES.f90:1448-1530, 4780-4862) */
+static void interp_matrix(const ctx* X, const int cell[3], double acos_mu, double sc[16]) {
+    const double pi = PI_;
+    double deg = acos_mu * 180.0 / pi;
+    int up, lo;
+    if (fmod(deg, 1.0) > 0.5) { up = (int)deg + 2; lo = (int)deg + 1; }
+    else { up = (int)deg + 1; lo = (int)deg; }
+    if (up == 1) { for (int i = 0; i < 16; i++) sc[i] = smat(X, cell, i + 1, 1); }
+    else if (lo == 180) { for (int i = 0; i < 16; i++) sc[i] = smat(X, cell, i + 1, 180); }
+    else {
+        for (int i = 0; i < 16; i++) {
+            double x0 = smat(X, cell, i + 1, lo), x1 = smat(X, cell, i + 1, up);
+            double y0 = (double)lo - 0.5, y1 = (double)up - 0.5;
+            sc[i] = (x1 - x0) * (deg - y0) / (y1 - y0) + x0;
+        }
+    }
+}
+
+/* scatter_photon (ARTES.f90:1434-1532) */
+static void scatter_photon(ctx* X, rng_t* rng, const double dir[3], const double st[4], const int cell[3],
+                           double dnew[3], double* alpha, double* beta, double sc[16]) {
+    X->cnt[ARTES_CNT_SCATTERS]++;
+    scattering_angle_sampling(X, rng, st, alpha, beta, cell);
+    direction_cosine(X, *alpha, *beta, dir, dnew);
+    interp_matrix(X, cell, acos(*alpha), sc);
+}
+
+/* packet-level second moment bookkeeping (plane 3 of the detector, totals[8]) */
+static void flush_pixel(ctx* X) {
+    if (X->cur_pix >= 0) {
+        size_t plane = (size_t)X->nx * X->ny;
+        for (int k = 0; k < 4; k++) X->detector[(3 * 4 + k) * plane + X->cur_pix] += X->cur_sum[k] * X->cur_sum[k];
+    }
+    X->cur_pix = -1;
+    for (int k = 0; k < 4; k++) X->cur_sum[k] = 0.0;
+}
+
+static void end_packet_stats(ctx* X) {
+    flush_pixel(X);
+    for (int k = 0; k < 4; k++) {
+        X->totals[k] += X->pkt_tot[k];
+        X->totals[4 + k] += X->pkt_tot[k] * X->pkt_tot[k];
+        X->pkt_tot[k] = 0.0;
+    }
+}
+
+/* peel_photon (ARTES.f90:4710-4990) */
+static void peel_photon(ctx* X, double xp, double yp, double zp, const double st[4], const double dirp[3],
+                        const int cell_in[3], const int face_in[2], int* cell_error) {
+    const double pi = PI_;
+    const double* det = X->det;
+    double x = xp, y = yp, z = zp, fd, tau_total = 0.0;
+    int cf[2] = {face_in[0], face_in[1]}, nf[2], cell[3] = {cell_in[0], cell_in[1], cell_in[2]}, cout[3], gexit = 0;
+    X->cnt[ARTES_CNT_PEELS]++;
+    *cell_error = 0;
+    for (;;) {
+        cell_face(X, x, y, z, det, cf, nf, &fd, &gexit, cell, cout, cell_error);
+        if (*cell_error) error_log(X, 43);
+        tau_total += fd * kappa(X, cell);
+        x += fd * det[0]; y += fd * det[1]; z += fd * det[2];
+        if (gexit || *cell_error || (nf[0] == 1 && nf[1] == X->cell_depth)) break;
+        cf[0] = nf[0]; cf[1] = nf[1];
+        cell[0] = cout[0]; cell[1] = cout[1]; cell[2] = cout[2];
+    }
+    if (*cell_error) return;
+    if (!(gexit && tau_total < 50.0)) return;
+    double w = exp(-tau_total);
+    double mu = dirp[0] * det[0] + dirp[1] * det[1] + dirp[2] * det[2];
+    if (mu >= 1.0) mu = 1.0 - 1.e-10;
+    else if (mu <= -1.0) mu = -1.0 + 1.e-10;
+    double sc[16], sout[4] = {0, 0, 0, 0};
+    interp_matrix(X, cell_in, acos(mu), sc);
+    double phi_old = atan2(dirp[1], dirp[0]);
+    if (phi_old < 0.0) phi_old += 2.0 * pi;
+    if (phi_old > 2.0 * pi) phi_old -= 2.0 * pi;
+    double phi_new = atan2(det[1], det[0]);
+    if (phi_new < 0.0) phi_new += 2.0 * pi;
+    if (phi_new > 2.0 * pi) phi_new -= 2.0 * pi;
+    int have_out = 0;
+    if (fabs(dirp[2]) < 1.0) {
+        double num = (det[2] - dirp[2] * mu) / (sqrt(1.0 - mu * mu) * sqrt(1.0 - dirp[2] * dirp[2]));
+        double phs = 0.0;
+        if (fabs(num) < 1.0) phs = acos(num);
+        else if (num >= 1.0) phs = 0.0 + 1.e-10;
+        else if (num <= -1.0) phs = pi - 1.e-10;
+        else error_log(X, 44);
+        if (phi_old - phi_new >= 0.0 && phi_old - phi_new < pi) phs = 2.0 * pi - phs;
+        if (2.0 * pi + phi_old - phi_new >= 0.0 && 2.0 * pi + phi_old - phi_new < pi) phs = 2.0 * pi - phs;
+        if (phs < 0.0) phs += 2.0 * pi;
+        if (fabs(mu) < 1.0) { polarization_rotation(X, mu, phs, st, sc, dirp, det, sout, 1); have_out = 1; }
+        else { error_log(X, 49); *cell_error = 1; }
+    } else {
+        error_log(X, 45);
+    }
+    if (*cell_error || !have_out) return;
+    double x_im = yp * X->cos_det_phi - xp * X->sin_det_phi;
+    double y_im = zp * X->sin_det_theta - yp * X->cos_det_theta * X->sin_det_phi - xp * X->cos_det_theta * X->cos_det_phi;
+    int ix = (int)((double)X->nx * (x_im + X->p->x_max) / (2.0 * X->p->x_max));
+    int iy = (int)((double)X->ny * (y_im + X->p->y_max) / (2.0 * X->p->y_max));
+    double wI = w * sout[0];
+    if (wI > 0.0 && wI < 1.e100) {
+        if (ix < 0 || ix >= X->nx || iy < 0 || iy >= X->ny) { error_log(X, 63); return; }
+        size_t plane = (size_t)X->nx * X->ny, pix = (size_t)iy * X->nx + ix;
+        double v[4] = {w * sout[0], -w * sout[1], w * sout[2], w * sout[3]};   /* -Q: ARTES.f90:4956 */
+        for (int k = 0; k < 4; k++) {
+            X->detector[(0 * 4 + k) * plane + pix] += v[k];
+            X->detector[(1 * 4 + k) * plane + pix] += v[k] * v[k];
+            X->detector[(2 * 4 + k) * plane + pix] += 1.0;
+            X->pkt_tot[k] += v[k];
+        }
+        if ((int)pix != X->cur_pix) {
+            flush_pixel(X);
+            X->cur_pix = (int)pix;
+        }
+        for (int k = 0; k < 4; k++) X->cur_sum[k] += v[k];
+        X->cnt[ARTES_CNT_DETECTED]++;
+        X->peel_sum += wI;
+    } else {
+        error_log(X, 53);
+    }
+}
+
+/* initial_cell (ARTES.f90:2605-2669), star branch */
+static void initial_cell(const ctx* X, double x, double y, double z, int cell[3]) {
+    const oracle_grid* g = X->g;
+    const double pi = PI_;
+    double r = sqrt(x * x + y * y + z * z);
+    double theta = acos(z / r);
+    double phi = atan2(y, x);
+    if (phi < 0.0) phi += 2.0 * pi;
+    cell[0] = g->nr - 1; cell[1] = 0; cell[2] = 0;
+    for (int j = 0; j < g->ntheta; j++)
+        if (theta > g->thetafront[j] && theta < g->thetafront[j + 1]) { cell[1] = j; break; }
+    for (int j = 0; j < g->nphi; j++) {
+        if (j < g->nphi - 1) { if (phi > g->phifront[j] && phi < g->phifront[j + 1]) { cell[2] = j; break; } }
+        else { if (phi > g->phifront[j] && phi < 2.0 * pi) { cell[2] = j; break; } }
+    }
+}
+
+static void rotation_matrix(int axis, double ang, double m[3][3]) {
+    double c = cos(ang), s = sin(ang);
+    memset(m, 0, sizeof(double) * 9);
+    if (axis == 1) { m[0][0] = 1; m[1][1] = c; m[1][2] = -s; m[2][1] = s; m[2][2] = c; }
+    else if (axis == 2) { m[0][0] = c; m[0][2] = s; m[1][1] = 1; m[2][0] = -s; m[2][2] = c; }
+    else { m[0][0] = c; m[0][1] = -s; m[1][0] = s; m[1][1] = c; m[2][2] = 1; }
+}
+
+/* emit_photon, star branch (ARTES.f90:1027-1115) */
+static void emit_star(ctx* X, rng_t* rng, double pos[3], double dir[3], int face[2], int cell[3]) {
+    const oracle_grid* g = X->g;
+    const double pi = PI_;
+    const double R = g->rfront[g->nr];
+    double r_disk, phi_disk, xi;
+    face[0] = 1; face[1] = g->nr;
+    if (X->p->phase_far) {
+        for (;;) { xi = rng_uniform(rng); r_disk = sqrt(xi); if (r_disk > 0.9) break; }
+        xi = rng_uniform(rng); phi_disk = 2.0 * pi * xi;
+    } else {
+        xi = rng_uniform(rng); r_disk = sqrt(xi);
+        xi = rng_uniform(rng); phi_disk = 2.0 * pi * xi;
+    }
+    double d1 = R * r_disk * sin(phi_disk), d2 = R * r_disk * cos(phi_disk);
+    dir[0] = -1.0; dir[1] = 0.0; dir[2] = 0.0;
+    pos[0] = sqrt(R * R - d1 * d1 - d2 * d2); pos[1] = d1; pos[2] = d2;
+    if (X->p->stellar_direction) {
+        double m[3][3], t[3];
+        rotation_matrix(2, -(pi / 2.0 - X->p->theta_star), m);
+        for (int i = 0; i < 3; i++) t[i] = pos[0] * m[i][0] + pos[1] * m[i][1] + pos[2] * m[i][2];
+        rotation_matrix(3, X->p->phi_star, m);
+        for (int i = 0; i < 3; i++) pos[i] = t[0] * m[i][0] + t[1] * m[i][1] + t[2] * m[i][2];
+        double td = pi - X->p->theta_star, pd = pi + X->p->phi_star;
+        if (td < 0.0) td += 2.0 * pi;
+        if (td > 2.0 * pi) td -= 2.0 * pi;
+        if (pd < 0.0) pd += 2.0 * pi;
+        if (pd > 2.0 * pi) pd -= 2.0 * pi;
+        dir[0] = sin(td) * cos(pd); dir[1] = sin(td) * sin(pd); dir[2] = cos(td);
+    }
+    initial_cell(X, pos[0], pos[1], pos[2], cell);
+}
+
+/* propagation to the next interaction (ARTES.f90:689-778 / 848-941).
+ * returns 0 = interaction reached, 1 = grid exit, 2 = surface absorbed, 3 = cell error */
+static int propagate(ctx* X, rng_t* rng, double pos[3], const double dir[3], int face[2], int cell[3], double tau,
+                     double st[4]) {
+    double fd, tau_run = 0.0;
+    int nf[2], cout[3], gexit, cerr;
+    (void)st;
+    for (;;) {
+        cell_face(X, pos[0], pos[1], pos[2], dir, face, nf, &fd, &gexit, cell, cout, &cerr);
+        if (cerr) { error_log(X, 3); return 3; }
+        double k = kappa(X, cell);
+        double tau_cell = fd * k;
+        if (tau_run + tau_cell > tau) {
+            double s = (tau - tau_run) / k;
+            pos[0] += s * dir[0]; pos[1] += s * dir[1]; pos[2] += s * dir[2];
+            face[0] = 0; face[1] = 0;
+            return 0;
+        }
+        pos[0] += fd * dir[0]; pos[1] += fd * dir[1]; pos[2] += fd * dir[2];
+        face[0] = nf[0]; face[1] = nf[1];
+        cell[0] = cout[0]; cell[1] = cout[1]; cell[2] = cout[2];
+        if (gexit) return 1;
+        if (nf[0] == 1 && nf[1] == X->cell_depth) {
+            double xi = rng_uniform(rng);
+            if (xi > X->p->surface_albedo) return 2;
+            /* Lambertian reflection (surface_albedo > 0) is not restated: DESIGN.md §8f */
+            error_log(X, 62);
+            return 3;
+        }
+        tau_run += tau_cell;
+    }
+}
+
+/* one packet of radiative_transfer (ARTES.f90:557-953). Returns end state. */
+static int transport_packet(ctx* X, uint64_t seed, uint64_t id, double* nscat_out) {
+    const artes_run_params* p = X->p;
+    rng_t rng;
+    rng_seed(&rng, seed, id);
+    double pos[3], dir[3], st[4] = {1.0, 0.0, 0.0, 0.0};
+    int face[2], cell[3];
+    X->cnt[ARTES_CNT_PACKETS]++;
+    X->peel_sum = 0.0;
+    *nscat_out = 0.0;
+    emit_star(X, &rng, pos, dir, face, cell);
+
+    /* optical depth to the boundary or the surface (ARTES.f90:625-656) */
+    double tau_first = 0.0, xc = pos[0], yc = pos[1], zc = pos[2], fd;
+    int cfc[2] = {face[0], face[1]}, cc[3] = {cell[0], cell[1], cell[2]}, nf[2] = {0, 0}, cout[3], gexit, cerr;
+    for (;;) {
+        cell_face(X, xc, yc, zc, dir, cfc, nf, &fd, &gexit, cc, cout, &cerr);
+        if (cerr) error_log(X, 2);
+        tau_first += fd * kappa(X, cc);
+        xc += fd * dir[0]; yc += fd * dir[1]; zc += fd * dir[2];
+        if (cerr || gexit || (nf[0] == 1 && nf[1] == X->cell_depth)) break;
+        cfc[0] = nf[0]; cfc[1] = nf[1];
+        cc[0] = cout[0]; cc[1] = cout[1]; cc[2] = cout[2];
+    }
+    double tau, xi;
+    int surf = (nf[0] == 1 && nf[1] == X->cell_depth);
+    if (tau_first < 1.e-6 && !surf) { X->cnt[ARTES_CNT_DROPPED]++; return 3; }
+    else if (tau_first < 1.e-6 && surf) { xi = rng_uniform(&rng); tau = -log(1.0 - xi); }
+    else {
+        xi = rng_uniform(&rng);
+        if (tau_first < 50.0) {
+            tau = -log(1.0 - xi * (1.0 - exp(-tau_first)));
+            for (int i = 0; i < 4; i++) st[i] *= (1.0 - exp(-tau_first));
+        } else tau = -log(1.0 - xi);
+    }
+    int r = propagate(X, &rng, pos, dir, face, cell, tau, st);
+    if (r == 1) { X->cnt[ARTES_CNT_EXITED]++; return 1; }
+    if (r == 2) { X->cnt[ARTES_CNT_ABSORBED]++; return 2; }
+    if (r == 3) { X->cnt[ARTES_CNT_DROPPED]++; return 3; }
+
+    /* scattering loop (ARTES.f90:788-951) */
+    for (;;) {
+        if (!p->photon_scattering) { X->cnt[ARTES_CNT_ABSORBED]++; return 2; }
+        xi = rng_uniform(&rng);
+        if (xi < p->fstop) { X->cnt[ARTES_CNT_ABSORBED]++; return 2; }
+        double alb = X->g->cell_albedo[(size_t)X->wl * X->g->ncell + cidx(X->g, cell)];
+        if (alb < 1.0 && alb > 0.0) {
+            double gamma = alb / (1.0 - p->fstop);
+            for (int i = 0; i < 4; i++) st[i] *= gamma;
+        }
+        if (st[0] <= p->photon_minimum) { X->cnt[ARTES_CNT_ABSORBED]++; return 2; }
+        peel_photon(X, pos[0], pos[1], pos[2], st, dir, cell, face, &cerr);
+        if (cerr) { X->cnt[ARTES_CNT_DROPPED]++; return 3; }
+        double dnew[3], alpha, beta, sc[16], snew[4];
+        scatter_photon(X, &rng, dir, st, cell, dnew, &alpha, &beta, sc);
+        *nscat_out += 1.0;
+        if (fabs(alpha) < 1.0) {
+            polarization_rotation(X, alpha, beta, st, sc, dir, dnew, snew, 0);
+            for (int i = 0; i < 4; i++) st[i] = snew[i];
+            dir[0] = dnew[0]; dir[1] = dnew[1]; dir[2] = dnew[2];
+        } else {
+            error_log(X, 50);
+            X->cnt[ARTES_CNT_DROPPED]++;
+            return 3;
+        }
+        xi = rng_uniform(&rng);
+        tau = -log(1.0 - xi);
+        r = propagate(X, &rng, pos, dir, face, cell, tau, st);
+        if (r == 1) { X->cnt[ARTES_CNT_EXITED]++; return 1; }
+        if (r == 2) { X->cnt[ARTES_CNT_ABSORBED]++; return 2; }
+        if (r == 3) { error_log(X, 5); X->cnt[ARTES_CNT_DROPPED]++; return 3; }
+    }
+}
+
+/* Run packets [first, first+n). detector [4][4][ny][nx], totals[8], counters, err are ACCUMULATED into.
+ * records (optional) [n][4] = {peeled I sum, scatters, crossings, end state}. */
+int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
+               int nthreads, double* detector, double* totals, uint64_t* counters, uint64_t* err, double* records) {
+    if (!g || !p || !detector) return -22;
+    if (p->photon_source != 1) return -38;
+    int cell_depth = p->cell_depth >= 0 ? p->cell_depth : oracle_cell_depth(g, p->wl_index);
+    size_t detn = (size_t)16 * p->nx * p->ny;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#else
+    nthreads = 1;
+#endif
+    double* dets = (double*)calloc(detn * (size_t)nthreads, sizeof(double));
+    uint64_t* cnts = (uint64_t*)calloc((size_t)ARTES_NUM_COUNTERS * nthreads, sizeof(uint64_t));
+    uint64_t* errs = (uint64_t*)calloc((size_t)ARTES_NUM_ERR * nthreads, sizeof(uint64_t));
+    double* tots = (double*)calloc((size_t)8 * nthreads, sizeof(double));
+    if (!dets || !cnts || !errs || !tots) { free(dets); free(cnts); free(errs); free(tots); return -12; }
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        int t = 0;
+#ifdef _OPENMP
+        t = omp_get_thread_num();
+#endif
+        ctx X;
+        memset(&X, 0, sizeof(X));
+        X.g = g; X.p = p; X.wl = p->wl_index; X.cell_depth = cell_depth; X.nx = p->nx; X.ny = p->ny;
+        X.det[0] = sin(p->det_theta) * cos(p->det_phi);      /* spherical_cartesian, ARTES.f90:495 */
+        X.det[1] = sin(p->det_theta) * sin(p->det_phi);
+        X.det[2] = cos(p->det_theta);
+        X.sin_det_theta = sin(p->det_theta); X.cos_det_theta = cos(p->det_theta);
+        X.sin_det_phi = sin(p->det_phi); X.cos_det_phi = cos(p->det_phi);
+        X.detector = dets + detn * t;
+        X.cnt = cnts + (size_t)ARTES_NUM_COUNTERS * t;
+        X.err = errs + (size_t)ARTES_NUM_ERR * t;
+        X.totals = tots + (size_t)8 * t;
+        X.cur_pix = -1;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (int64_t i = 0; i < (int64_t)n; i++) {
+            uint64_t c0 = X.cnt[ARTES_CNT_CROSSINGS];
+            double nscat = 0.0;
+            int endst = transport_packet(&X, seed, first + (uint64_t)i, &nscat);
+            end_packet_stats(&X);
+            if (records) {
+                double* rec = records + (size_t)i * 4;
+                rec[0] = X.peel_sum;
+                rec[1] = nscat;
+                rec[2] = (double)(X.cnt[ARTES_CNT_CROSSINGS] - c0);
+                rec[3] = (double)endst;
+            }
+        }
+    }
+    for (int t = 0; t < nthreads; t++) {
+        for (size_t i = 0; i < detn; i++) detector[i] += dets[detn * t + i];
+        if (counters) for (int i = 0; i < ARTES_NUM_COUNTERS; i++) counters[i] += cnts[(size_t)ARTES_NUM_COUNTERS * t + i];
+        if (err) for (int i = 0; i < ARTES_NUM_ERR; i++) err[i] += errs[(size_t)ARTES_NUM_ERR * t + i];
+        if (totals) for (int i = 0; i < 8; i++) totals[i] += tots[(size_t)8 * t + i];
+    }
+    free(dets); free(cnts); free(errs); free(tots);
+    return 0;
+}
+
+int oracle_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

@@ -1,0 +1,83 @@
+"""ctypes binding of the CPU oracle (oracle/artes_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+See the header of artes_oracle.c for what the oracle restates and how it is pinned.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from artes_amd.abi import ARTES_NUM_COUNTERS, ARTES_NUM_ERR, GridArrays, GridDesc, RunParams
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        L.oracle_grid_create.restype = C.c_void_p
+        L.oracle_grid_create.argtypes = [C.POINTER(GridDesc)]
+        L.oracle_grid_destroy.argtypes = [C.c_void_p]
+        L.oracle_cell_depth.restype = C.c_int
+        L.oracle_cell_depth.argtypes = [C.c_void_p, C.c_int]
+        L.oracle_run.restype = C.c_int
+        L.oracle_run.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
+                                 C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        L.oracle_max_threads.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+class OracleGrid:
+    def __init__(self, atm: dict, oblateness: float = 0.0):
+        self.arrays = GridArrays(atm, oblateness)
+        self.h = lib().oracle_grid_create(C.byref(self.arrays.desc))
+        if not self.h:
+            raise MemoryError("oracle_grid_create failed")
+
+    def cell_depth(self, wl: int = 0) -> int:
+        return lib().oracle_cell_depth(self.h, wl)
+
+    def run(self, params: RunParams, first: int, n: int, seed: int, threads: int = 0, records: bool = False):
+        det = np.zeros((4, 4, params.ny, params.nx))
+        tot = np.zeros(8)
+        cnt = np.zeros(ARTES_NUM_COUNTERS, dtype=np.uint64)
+        err = np.zeros(ARTES_NUM_ERR, dtype=np.uint64)
+        rec = np.zeros((n, 4)) if records else None
+        rc = lib().oracle_run(self.h, C.byref(params), first, n, seed, threads,
+                              det.ctypes.data_as(C.POINTER(C.c_double)), tot.ctypes.data_as(C.POINTER(C.c_double)),
+                              cnt.ctypes.data_as(C.POINTER(C.c_uint64)), err.ctypes.data_as(C.POINTER(C.c_uint64)),
+                              rec.ctypes.data_as(C.POINTER(C.c_double)) if rec is not None else None)
+        if rc != 0:
+            raise RuntimeError(f"oracle_run failed: {rc}")
+        return det, tot, cnt, err, rec
+
+    def close(self):
+        if self.h:
+            lib().oracle_grid_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def max_threads() -> int:
+    return lib().oracle_max_threads()
