@@ -1,0 +1,92 @@
+"""Multi-GPU execution: one process per GPU, packets sharded, one RCCL sum-reduce.
+
+The reference parallelises only over packets with OpenMP and sums per-thread detector
+copies serially after the loop (``ARTES.f90:534-546``, ``959-975``).  Here each rank
+transports the disjoint global packet range ``[k*N/G, (k+1)*N/G)`` on its own GPU (the
+RNG is keyed by the global packet id, so the result does not depend on G), and the
+detector tensor ``[4][4][ny][nx]`` (plus 8 packet-level moments, counters and error
+codes) is summed with ONE ``all_reduce`` per (wavelength, detector direction)
+(SURVEY.md §5, §8e).  The payload is ~80 KB at 25x25 pixels: latency-bound, so a
+single flat RCCL all-reduce over xGMI is the whole exchange.
+
+``torch.distributed`` with backend ``nccl`` is RCCL on ROCm; ``gloo`` is used for the
+CPU tests of this module.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class Rank:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+
+
+def env_rank() -> Rank:
+    return Rank(int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+                int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def init(backend: str | None = None) -> Rank:
+    """Initialise torch.distributed from the torchrun environment (no-op for one process)."""
+    r = env_rank()
+    if r.world > 1:
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            if backend is None:
+                import torch
+
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            kw = {}
+            if backend == "nccl":
+                import torch
+
+                torch.cuda.set_device(r.local_rank)
+                kw["device_id"] = torch.device("cuda", r.local_rank)
+            dist.init_process_group(backend=backend, rank=r.rank, world_size=r.world, **kw)
+    return r
+
+
+def shard(n_packets: int, rank: int, world: int) -> tuple[int, int]:
+    """Global packet range of ``rank``: ``[k*N//G, (k+1)*N//G)``, as (first, count)."""
+    lo = (n_packets * rank) // world
+    hi = (n_packets * (rank + 1)) // world
+    return lo, hi - lo
+
+
+def allreduce_numpy(arrays: list[np.ndarray], world: int) -> list[np.ndarray]:
+    """Sum host arrays over ranks (gloo / CPU path)."""
+    if world <= 1:
+        return arrays
+    import torch
+    import torch.distributed as dist
+
+    out = []
+    for a in arrays:
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        out.append(t.numpy().astype(a.dtype, copy=False) if a.dtype != np.float64 else t.numpy())
+    return out
+
+
+def run_sharded(transport, n_packets: int, seed: int, r: Rank):
+    """Run ``transport(first, count, seed) -> RunResult`` on this rank's shard and sum
+    the results over all ranks (host tensors; the GPU bench uses device tensors + RCCL)."""
+    first, count = shard(n_packets, r.rank, r.world)
+    res = transport(first, count, seed)
+    if r.world > 1:
+        det, tot, cnt, err = allreduce_numpy([res.det, res.totals, res.counters.astype(np.float64),
+                                              res.err.astype(np.float64)], r.world)
+        res.det, res.totals = det, tot
+        res.counters = np.rint(cnt).astype(np.uint64)
+        res.err = np.rint(err).astype(np.uint64)
+    return res

@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: photon packets per second on the BASELINE.json headline configuration.
+
+Workload (BASELINE.json configs[2]): Rayleigh-polarised atmosphere (full 16-element
+Mueller matrix), 32 x 16 x 32 (r, theta, phi) cells, one wavelength, star source,
+imaging_mono 25 x 25 detector at theta = phi = 90 deg, radial tau = 1, albedo 1.
+One step = one `radiative_transfer` call (ARTES.f90:518-1006) of `--packets` packets
+per GPU (default 1e9 = the config's packet count), followed by the RCCL sum-reduce of
+the detector over ranks.  Weak scaling: every GPU transports `--packets` per step.
+
+Run:   python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+           --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+Prints ONE JSON line (rank 0).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# canonical algorithmic bytes per packet: 8 B of kappa per crossing,
+# 304 B per scatter (albedo 8 + p1j 32 + two 16-element f64 rows 256 + ...), 352 B per
+# peel (two matrix rows 256 + 12-value detector read-modify-write 96)
+B_PER_CROSSING, B_PER_SCATTER, B_PER_PEEL = 8.0, 304.0, 352.0
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+
+
+def cpu_baseline(atm, params, budget_s: float = 15.0) -> dict:
+    """The CPU oracle (C restatement of the reference packet loop, OpenMP) on host cores."""
+    from oracle import oracle
+
+    threads = int(os.environ.get("ARTES_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    g = oracle.OracleGrid(atm)
+    probe = 20000
+    t0 = time.perf_counter()
+    g.run(params, 0, probe, 99, threads=threads)
+    rate = probe / max(time.perf_counter() - t0, 1e-6)
+    n = int(min(max(rate * budget_s, 1e5), 5e7))
+    t0 = time.perf_counter()
+    g.run(params, 10**12, n, 99, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mphotons/s", "cores": threads, "kind": "port",
+            "sample": f"{n} packets of the same ray3d workload (oracle/artes_oracle.c, {threads} OpenMP threads, {dt:.1f} s)"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--packets", type=float, default=1e9, help="packets per GPU per step")
+    ap.add_argument("--seed", type=int, default=20171015)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from artes_amd import dist, driver, stats, synthetic
+    from artes_amd.engine import Grid
+
+    r = dist.init()
+    world = r.world
+    dev = r.local_rank
+    torch.cuda.set_device(dev)
+    per_gpu = int(args.packets)
+
+    cfg = driver.default_config()
+    # the survey's inputs for the frozen reference runs (tests/golden/README.md)
+    atm = synthetic.make_config("ray3d", normalizer="simpson")
+    rtop = float(atm["radial"][-1])
+    det_geom = driver.detector_geometry(cfg, rtop)
+    grid = Grid(atm, device=dev)
+    params = driver.run_params(cfg, det_geom, 0, cell_depth=grid.cell_depth(0))
+    ny, nx = det_geom.ny, det_geom.nx
+
+    f64 = dict(dtype=torch.float64, device=f"cuda:{dev}")
+    det = torch.zeros((4, 4, ny, nx), **f64)
+    tot2 = torch.zeros(4, **f64)
+    cnt = torch.zeros(8, dtype=torch.int64, device=f"cuda:{dev}")
+    err = torch.zeros(64, dtype=torch.int64, device=f"cuda:{dev}")
+    stream = torch.cuda.current_stream()
+
+    def step(k: int):
+        det.zero_(); tot2.zero_(); cnt.zero_(); err.zero_()
+        first = (k * world + r.rank) * per_gpu
+        grid.run_device(params, first, per_gpu, args.seed, det.data_ptr(), tot2.data_ptr(), cnt.data_ptr(),
+                        err.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            import torch.distributed as tdist
+
+            tdist.all_reduce(det)
+            tdist.all_reduce(tot2)
+            tdist.all_reduce(cnt)
+            tdist.all_reduce(err)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            import torch.distributed as tdist
+
+            tdist.barrier()
+        torch.cuda.synchronize()
+
+    for k in range(args.warmup):
+        step(k)
+    barrier()
+    ev = []
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step(args.warmup + k)          # the transport kernel runs on `stream`; all_reduce follows
+        e1.record(stream)
+        ev.append((e0, e1))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    # transport duration per launch, HIP events on the launch stream, over the timed region
+    # (the step's events bracket run_device and the RCCL reduce; the library's own events
+    # bracket the transport kernel alone for the last launch)
+    step_ms = [a.elapsed_time(b) for a, b in ev]
+    kernel_only_ms = grid.last_kernel_ms()
+    if world > 1:
+        import torch.distributed as tdist
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if r.rank != 0:
+        if world > 1:
+            import torch.distributed as tdist
+
+            tdist.barrier()
+        return 0
+
+    total_packets = per_gpu * world * args.steps
+    value = total_packets / elapsed / 1e6
+    cnt_h = cnt.cpu().numpy().astype(np.float64)
+    n_step = per_gpu * world
+    C = cnt_h[0] / n_step
+    S = cnt_h[1] / n_step
+    P = cnt_h[2] / n_step
+    b_alg = B_PER_CROSSING * C + B_PER_SCATTER * S + B_PER_PEEL * P
+    k_ms = float(np.mean(step_ms))
+    achieved = b_alg * per_gpu / (k_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            pmc = json.load(open(args.pmc_json))
+            traffic = float(pmc["hbm_bytes_per_packet"]) * per_gpu
+        except Exception:
+            traffic = None
+
+    # Stokes-I parity against the frozen reference run (tests/golden)
+    parity = None
+    ref_dir = os.path.join(ROOT, "tests", "golden", "reference_runs", "t_ray3d_ARTES_det_1e6")
+    if os.path.isdir(ref_dir):
+        raw = det.cpu().numpy()
+        E = driver.package_energy(cfg, float(atm["wavelength"][0]) * 1e-6, rtop, n_step, det_geom.det_phi)
+        cmp = stats.compare_to_reference(raw, n_step, E, det_geom.pixel_scale, stats.load_reference_run(ref_dir), 10**6)
+        ph = driver.photometry(driver.scale_detector(raw[:3], E))
+        ref_ph = stats.load_reference_run(ref_dir)["photometry"]
+        parity = {"stokes_I_rms_z": round(cmp["rms_z"], 4), "stokes_I_mean_z": round(cmp["mean_z"], 4),
+                  "pixels": cmp["n_pixels"], "I_total": ph[0] * 1e-6, "I_total_reference": float(ref_ph[1]),
+                  "reference": "tests/golden/reference_runs/t_ray3d_ARTES_det_1e6 (1e6 packets)"}
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(atm, params)
+
+    out = {
+        "metric": json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"],
+        "value": round(value, 3),
+        "unit": "Mphotons/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (uniform Rayleigh atmosphere, generated in-process; no checkpoint/dataset)",
+        "config": {"workload": "BASELINE configs[2]: Rayleigh 16-element Mueller, 32x16x32 (r,theta,phi), 1 wavelength, "
+                               "star source, imaging_mono 25x25, tau=1",
+                   "packets_per_gpu_per_step": per_gpu, "parallelism": f"packet-sharded x{world}, RCCL detector all-reduce"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "kernel_ms": round(k_ms, 3), "transport_kernel_ms_last": round(kernel_only_ms, 3),
+                     "bytes_per_packet_alg": round(b_alg, 1),
+                     "events_per_packet": {"crossings": round(C, 3), "scatters": round(S, 4), "peels": round(P, 4)}},
+        "cpu_baseline": cpu,
+        "parity": parity,
+        "errors": {str(i): int(e) for i, e in enumerate(err.cpu().numpy()) if e},
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as tdist
+
+        tdist.barrier()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

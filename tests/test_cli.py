@@ -1,0 +1,97 @@
+"""End-to-end drop-in CLI: input/<atm>/{artes.in,atmosphere.fits} -> output/<run>/...
+
+The CPU tests inject the oracle as the per-rank transport to exercise the host-side
+plumbing (argv grammar, directory handling, output formats); the GPU test drives the
+real engine."""
+
+import os
+
+import numpy as np
+import pytest
+
+from artes_amd import atmosphere, fitsio, runner, synthetic
+from artes_amd.engine import RunResult
+
+ARTES_IN = """======================================
+* ARTES input parameters
+photon:source=star
+photon:fstop=1d-5
+photon:minimum=1d-20
+star:temperature=5800
+star:radius=1
+planet:orbit=5
+detector:type={mode}
+detector:theta=90
+detector:phi=90
+detector:pixel=25
+detector:distance=10
+"""
+
+
+def _make_input(root, mode="imaging_mono", name="ray3d", **spec):
+    d = root / "input" / "atm"
+    d.mkdir(parents=True)
+    (d / "artes.in").write_text(ARTES_IN.format(mode=mode))
+    atm = synthetic.make_config(name, **spec)
+    atmosphere.write_atmosphere_fits(str(d / "atmosphere.fits"), atm)
+    return d
+
+
+class OracleTransport:
+    def __init__(self, atm, device, oblateness):
+        from oracle.oracle import OracleGrid
+
+        self.g = OracleGrid(atm, oblateness)
+
+    def cell_depth(self, wl):
+        return self.g.cell_depth(wl)
+
+    def run(self, params, first, n, seed):
+        d, t, c, e, _ = self.g.run(params, first, n, seed, threads=4)
+        return RunResult(d, t, c, e)
+
+
+def test_usage_and_missing_input(tmp_path, capsys):
+    assert runner.run([], root=str(tmp_path)) == 0
+    assert "How to run ARTES" in capsys.readouterr().out
+    assert runner.run(["nope", "1000"], root=str(tmp_path)) == 0
+
+
+def test_imaging_mono_outputs_cpu_plumbing(tmp_path):
+    _make_input(tmp_path, nr=6, ntheta=4, nphi=4)
+    rc = runner.run(["atm", "2e4", "-o", "run1", "-k", "photon:fstop=2d-5", "--seed", "5"], root=str(tmp_path),
+                    transport_factory=OracleTransport)
+    assert rc == 0
+    out = tmp_path / "output" / "run1"
+    for f in ("error.log", "plot.dat", "input/artes.in", "input/atmosphere.fits", "output/stokes.fits",
+              "output/error.fits", "output/photometry.dat", "output/normalization.dat", "output/cell_depth.dat"):
+        assert (out / f).exists(), f
+    assert (out / "input" / "artes.in").read_text().rstrip().endswith("photon:fstop=2d-5")
+    s = fitsio.read(out / "output" / "stokes.fits")[0].data
+    assert s.shape == (4, 25, 25) and s[0].sum() > 0
+
+
+def test_spectrum_and_phase_modes(tmp_path):
+    _make_input(tmp_path, mode="spectrum", name="iso", wavelength=(0.5, 0.7, 0.9))
+    assert runner.run(["atm", "5e3", "-o", "spec", "--seed", "1"], root=str(tmp_path), transport_factory=OracleTransport) == 0
+    lines = [l for l in (tmp_path / "output/spec/output/spectrum.dat").read_text().splitlines() if l.strip() and "#" not in l]
+    assert len(lines) == 3 and float(lines[1].split()[0]) == pytest.approx(0.7)
+    import shutil
+
+    shutil.rmtree(tmp_path / "input")
+    _make_input(tmp_path, mode="phase", name="iso")
+    assert runner.run(["atm", "2e3", "-o", "ph", "--seed", "1"], root=str(tmp_path), transport_factory=OracleTransport) == 0
+    rows = [l for l in (tmp_path / "output/ph/output/phase.dat").read_text().splitlines() if l.strip() and "#" not in l]
+    assert len(rows) == 73 and float(rows[0].split()[0]) == 0.0 and float(rows[-1].split()[0]) == 180.0
+
+
+@pytest.mark.gpu
+def test_cli_on_gpu(tmp_path, require_gpu):
+    _make_input(tmp_path, share_matrix=False)
+    assert runner.run(["atm", "1e7", "-o", "gpu", "--seed", "3"], root=str(tmp_path)) == 0
+    ph = open(tmp_path / "output/gpu/output/photometry.dat").read()
+    from artes_amd.stats import read_photometry
+
+    v = read_photometry(str(tmp_path / "output/gpu/output/photometry.dat"))
+    assert v[1] == pytest.approx(2.503e-19, rel=0.01) and v[3] < 0
+    assert os.path.getsize(tmp_path / "output/gpu/error.log") == 0

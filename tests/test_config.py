@@ -1,0 +1,54 @@
+import math
+
+import pytest
+
+from artes_amd.config import AU, PC, R_SUN, ConfigError, RunConfig, is_comment, read_artes_in, split_key_value
+
+
+def test_defaults_match_reference():
+    c = RunConfig()      # ARTES.f90:280-314
+    assert c.photon_source == 1 and c.fstop == 1e-5 and c.photon_minimum == 1e-20
+    assert c.nx == c.ny == 25 and c.orbit == 5 * AU and c.distance_planet == 10 * PC
+    assert c.det_theta == 90.0 and c.det_phi == 90.0    # un-converted reference defaults
+
+
+def test_keywords_and_units():
+    c = RunConfig()
+    for k, v in [("photon:fstop", "1d-5"), ("photon:minimum", "1D-20"), ("star:radius", "2"),
+                 ("planet:orbit", "0.05"), ("detector:theta", "90"), ("detector:phi", "45"),
+                 ("detector:pixel", "11"), ("detector:distance", "3"), ("detector:type", "spectrum"),
+                 ("photon:scattering", "off"), ("general:log", "on")]:
+        c.apply(k, v)
+    assert c.fstop == 1e-5 and c.photon_minimum == 1e-20
+    assert c.r_star == 2 * R_SUN and c.orbit == pytest.approx(0.05 * AU)
+    assert c.det_theta == pytest.approx(math.pi / 2) and c.det_phi == pytest.approx(math.pi / 4)
+    assert c.nx == c.ny == 11 and c.mode == "spectrum" and not c.photon_scattering and c.log_file
+
+
+def test_clamps_and_order_dependence():
+    c = RunConfig()
+    c.apply("detector:theta", "0")
+    assert c.det_theta == 1e-3                               # ARTES.f90:4470
+    c.apply("detector:theta", "180")
+    assert c.det_theta == pytest.approx(math.pi - 1e-3)
+    c.apply("star:theta", "30")                              # ignored: star:direction not on yet
+    assert c.theta_star == pytest.approx(math.pi / 2)
+    c.apply("star:direction", "on")
+    c.apply("star:theta", "30")
+    assert c.theta_star == pytest.approx(math.pi / 6)
+
+
+def test_unknown_key_is_fatal():
+    with pytest.raises(ConfigError, match="Wrong keyword"):
+        RunConfig().apply("detector:foo", "1")
+
+
+def test_line_rules(tmp_path):
+    assert is_comment("* comment") and is_comment("-----") and is_comment("====") and is_comment("   ")
+    assert not is_comment("photon:fstop=1")
+    assert split_key_value("general:email='a@b.c'") == ("general:email", "a@b.c")
+    assert split_key_value('x="y"') == ("x", "y")
+    p = tmp_path / "artes.in"
+    p.write_text("* header\n\nphoton:fstop=1d-4\n----\ndetector:pixel=7\nstar:theta=\n")
+    c = read_artes_in(str(p))
+    assert c.fstop == 1e-4 and c.nx == 7
