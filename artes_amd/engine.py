@@ -34,6 +34,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise EngineUnavailable(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (soname
+    # libamdhip64.so.7).  Loading torch first makes this library's DT_NEEDED resolve to
+    # that same runtime, so torch tensors / RCCL and the engine share one HSA context.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     L = C.CDLL(LIB_PATH)
     L.artes_abi_version.restype = C.c_int32
     L.artes_build_info.restype = C.c_char_p
