@@ -1,0 +1,453 @@
+// device_common.hpp -- device-side building blocks shared by the transport kernels:
+// grid/run descriptors, the per-packet RNG, bounded sin/cos, the cell-face geometry
+// (ARTES.f90:2671-3470) and the scattering physics (ARTES.f90:1434-2052).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "tables.hpp"
+
+namespace artes {
+
+constexpr int NCOPY = 8;
+constexpr int BLOCK = 256;
+constexpr double PI = 3.14159265358979323846;
+constexpr double HALF_PI = PI / 2.0;
+constexpr double TWO_PI = 2.0 * PI;
+
+// -------------------------------------------------------------- device data ---
+struct DevGrid {
+    int nr, ntheta, nphi, ncell;
+    int cell_depth;
+    double ax2, by2, cz2, a, b;
+    double rtop;
+    const double* __restrict__ rf2;      // [nr+1]
+    const double* __restrict__ thetaf;   // [ntheta+1]
+    const double* __restrict__ tan2;     // [ntheta+1]
+    const int* __restrict__ tplane;      // [ntheta+1]
+    const double* __restrict__ phif;     // [nphi]
+    const double* __restrict__ phis;     // [nphi]
+    const double* __restrict__ phic;     // [nphi]
+    const double* __restrict__ kappa;    // [ncell] (this wavelength)
+    const double* __restrict__ albedo;   // [ncell]
+    const int* __restrict__ matid;       // [ncell]
+    const double* __restrict__ mats;     // [nmat][180][16]
+    const double* __restrict__ cums;     // [nmat][181][4]
+    const double* __restrict__ sc2;      // [181]
+    const double* __restrict__ ss2;      // [181]
+};
+
+struct DevRun {
+    uint64_t first, n, seed;
+    int nx, ny, photon_scattering, phase_far, stellar_direction, defer;
+    double det0, det1, det2, sdt, cdt, sdp, cdp;
+    double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
+    double* __restrict__ det;       // [NCOPY][4][4][ny][nx]
+    size_t det_stride;              // doubles per copy
+    double* __restrict__ tot2;      // [4] packet-level sum T^2 per Stokes
+    unsigned long long* __restrict__ cnt;   // [ARTES_NUM_COUNTERS]
+    unsigned long long* __restrict__ err;   // [ARTES_NUM_ERR]
+    double* __restrict__ rec;       // [n][4] (TRACE builds)
+};
+
+// ------------------------------------------------------------------- RNG ---
+// One xoroshiro128++ stream per global packet id; identical to oracle/artes_oracle.c.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t& x) {
+    uint64_t z = (x += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+struct Rng {
+    uint64_t s0, s1;
+    __device__ __forceinline__ void seed(uint64_t seed, uint64_t id) {
+        uint64_t k = seed;
+        uint64_t sm = splitmix64(k) + 2ULL * id * 0x9e3779b97f4a7c15ULL;
+        s0 = splitmix64(sm);
+        s1 = splitmix64(sm);
+        if ((s0 | s1) == 0) s1 = 1;
+    }
+    __device__ __forceinline__ double uni() {
+        const uint64_t a = s0;
+        uint64_t b = s1;
+        const uint64_t res = rotl64(a + b, 17) + a;
+        b ^= a;
+        s0 = rotl64(a, 49) ^ b ^ (b << 21);
+        s1 = rotl64(b, 28);
+        return ((double)(res >> 11) + 0.5) * 0x1.0p-53;
+    }
+};
+
+__device__ __forceinline__ void log_err(const DevRun& R, int code) { atomicAdd(&R.err[code], 1ULL); }
+
+// sin/cos for |x| <~ 1e5 (every angle here is < 4 pi): two-constant Cody-Waite reduction
+// by pi/2 with FMA, fdlibm __kernel_sin/__kernel_cos minimax polynomials on [-pi/4, pi/4].
+// Absolute error ~1e-16; avoids the Payne-Hanek path (and its registers) of ocml cos/sin.
+__device__ __forceinline__ void sincos_bounded(double x, double& s, double& c) {
+    const double n = rint(x * 0.63661977236758134308);
+    double r = fma(-n, 1.57079632679489655800e+00, x);
+    r = fma(-n, 6.12323399573676603587e-17, r);
+    const double z = r * r;
+    const double ps = z * (8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 + z * (2.75573137070700676789e-06 +
+                      z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10))));
+    const double sr = r + r * z * (-1.66666666666666324348e-01 + ps);
+    const double pc = z * z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * (2.48015872894767294178e-05 +
+                      z * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + pc);
+    const int q = ((int)n) & 3;
+    s = (q == 0) ? sr : (q == 1) ? cr : (q == 2) ? -sr : -cr;
+    c = (q == 0) ? cr : (q == 1) ? -sr : (q == 2) ? -cr : sr;
+}
+__device__ __forceinline__ double cos_b(double x) { double s, c; sincos_bounded(x, s, c); return c; }
+__device__ __forceinline__ double sin_b(double x) { double s, c; sincos_bounded(x, s, c); return s; }
+
+// ------------------------------------------------------------- geometry ---
+// quadratic_equation (ARTES.f90:4154-4173)
+__device__ __forceinline__ void quad_roots(double a, double b, double c, double& s0, double& s1) {
+    s0 = 0.0;
+    s1 = 0.0;
+    const double disc = b * b - 4.0 * a * c;
+    if (disc >= 0.0) {
+        const double q = -0.5 * (b + copysign(sqrt(disc), b));
+        if (fabs(a) > 1.e-100) s0 = q / a;
+        if (fabs(q) > 1.e-100) s1 = c / q;
+    }
+}
+// root selection block of cell_face (e.g. ARTES.f90:2897-2907)
+__device__ __forceinline__ double pick_root(double s0, double s1, double tol) {
+    if (s0 > tol && s1 <= tol && s0 < 1.e100) return s0;
+    if (s1 > tol && s0 <= tol && s1 < 1.e100) return s1;
+    if (s0 > tol && s1 > tol) {
+        if (s0 < 1.e100 && s0 < s1) return s0;
+        if (s1 < 1.e100 && s1 < s0) return s1;
+    }
+    return 0.0;
+}
+
+// theta cone x^2+y^2 = z^2 tan^2(theta_f) with the nappe filter (ARTES.f90:3026-3064)
+__device__ __forceinline__ double cone_distance(const DevGrid& G, int f, double x, double y, double z,
+                                                double n0, double n1, double n2, double tol) {
+    const double t2 = G.tan2[f];
+    const double qa = G.ax2 * n0 * n0 + G.by2 * n1 * n1 - G.cz2 * n2 * n2 * t2;
+    const double qb = 2.0 * (G.ax2 * x * n0 + G.by2 * y * n1 - G.cz2 * z * n2 * t2);
+    const double qc = G.ax2 * x * x + G.by2 * y * y - G.cz2 * z * z * t2;
+    double s0, s1;
+    quad_roots(qa, qb, qc, s0, s1);
+    const double th = G.thetaf[f];
+    if (s0 > 1.e-15) {
+        const double zt = z + s0 * n2;
+        if ((zt > 0.0 && th > HALF_PI) || (zt < 0.0 && th < HALF_PI)) s0 = 0.0;
+    }
+    if (s1 > 1.e-15) {
+        const double zt = z + s1 * n2;
+        if ((zt > 0.0 && th > HALF_PI) || (zt < 0.0 && th < HALF_PI)) s1 = 0.0;
+    }
+    return pick_root(s0, s1, tol);
+}
+
+struct Step {
+    double d;
+    int nft, nfi, ncr, nct, ncp;
+    bool exit, err;
+};
+
+// cell_face + next_cell (ARTES.f90:2671-3470) in a uniform form: every cell has an
+// inner and an outer face per coordinate; "same face" re-crossings of the face the
+// packet sits on use the reference's 1e-3 tolerance in the matching slot.  The
+// candidate set, tolerances and two-pass (>1e-9, then >1e-12) selection are the
+// reference's; DESIGN.md §3 walks through the equivalence.
+template <bool G3D>
+__device__ __forceinline__ void cell_face(const DevGrid& G, const DevRun& R, double x, double y, double z,
+                                          double n0, double n1, double n2, int ft, int fi, int cr, int ct, int cp,
+                                          Step& o) {
+    const double qa = G.ax2 * n0 * n0 + G.by2 * n1 * n1 + G.cz2 * n2 * n2;
+    const double qb = 2.0 * (G.ax2 * x * n0 + G.by2 * y * n1 + G.cz2 * z * n2);
+    const double S = G.ax2 * x * x + G.by2 * y * y + G.cz2 * z * z;
+    double s0, s1;
+    double d_rin = 0.0, d_rout = 0.0;
+    if (!(ft == 1 && fi == cr)) {                      // inner sphere r_cell
+        quad_roots(qa, qb, S - G.rf2[cr], s0, s1);
+        d_rin = pick_root(s0, s1, 1.e-15);
+    }
+    {                                                  // outer sphere r_cell+1 (same face: 1e-3)
+        quad_roots(qa, qb, S - G.rf2[cr + 1], s0, s1);
+        d_rout = pick_root(s0, s1, (ft == 1 && fi == cr + 1) ? 1.e-3 : 1.e-15);
+    }
+    double d_tin = 0.0, d_tout = 0.0, d_pin = 0.0, d_pout = 0.0;
+    int pout = 0;
+    if constexpr (G3D) {
+        const bool on_t = (ft == 2);
+        if (ct != 0) {                                 // inner theta face (index ct)
+            if (on_t && fi == ct) {
+                if (G.thetaf[ct] > HALF_PI && G.tplane[ct] == 1) d_tin = cone_distance(G, ct, x, y, z, n0, n1, n2, 1.e-3);
+            } else if (G.tplane[ct] == 1) {
+                d_tin = cone_distance(G, ct, x, y, z, n0, n1, n2, 1.e-15);
+            } else {
+                if (-z / n2 > 0.0 && n2 > 1.e-15) d_tin = -z / n2;
+            }
+        }
+        if (ct + 1 != G.ntheta) {                      // outer theta face (index ct+1)
+            if (on_t && fi == ct + 1) {
+                if (G.thetaf[ct + 1] < HALF_PI && G.tplane[ct + 1] == 1) d_tout = cone_distance(G, ct + 1, x, y, z, n0, n1, n2, 1.e-3);
+            } else if (G.tplane[ct + 1] == 1) {
+                d_tout = cone_distance(G, ct + 1, x, y, z, n0, n1, n2, 1.e-15);
+            } else {
+                if (-z / n2 > 0.0 && n2 < -1.e-15) d_tout = -z / n2;
+            }
+        }
+        if (G.nphi > 1) {                              // phi half-planes (ARTES.f90:3292-3350)
+            pout = (cp + 1 == G.nphi) ? 0 : cp + 1;
+            const bool on_p = (ft == 3);
+            double sp0 = 0.0;
+            if (!(on_p && fi == cp)) {
+                const double den = G.b * n1 * G.phic[cp] - G.a * n0 * G.phis[cp];
+                if (fabs(den) > 0.0) {
+                    sp0 = (G.a * x * G.phis[cp] - G.b * y * G.phic[cp]) / den;
+                    if (sp0 > 1.e-15 && sp0 < 1.e100) d_pin = sp0;
+                }
+            }
+            if (!(on_p && fi == pout)) {
+                const double den = G.b * n1 * G.phic[pout] - G.a * n0 * G.phis[pout];
+                if (fabs(den) > 0.0) {
+                    const double sp1 = (G.a * x * G.phis[pout] - G.b * y * G.phic[pout]) / den;
+                    if (sp1 > 1.e-15 && sp0 < 1.e100) d_pout = sp1;   // sic: sp0 (ARTES.f90:3318, 3346)
+                }
+            }
+        }
+    }
+    // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
+    double best = 1.e100;
+    int which = -1;
+#define ARTES_CONSIDER(dd, w, thr) if ((dd) > (thr) && (dd) < best) { best = (dd); which = (w); }
+    ARTES_CONSIDER(d_rin, 0, 1.e-9)
+    if constexpr (G3D) { ARTES_CONSIDER(d_tin, 1, 1.e-9) ARTES_CONSIDER(d_pin, 2, 1.e-9) }
+    ARTES_CONSIDER(d_rout, 3, 1.e-9)
+    if constexpr (G3D) { ARTES_CONSIDER(d_tout, 4, 1.e-9) ARTES_CONSIDER(d_pout, 5, 1.e-9) }
+    if (which < 0) {
+        best = 1.e100;
+        ARTES_CONSIDER(d_rin, 0, 1.e-12)
+        if constexpr (G3D) { ARTES_CONSIDER(d_tin, 1, 1.e-12) ARTES_CONSIDER(d_pin, 2, 1.e-12) }
+        ARTES_CONSIDER(d_rout, 3, 1.e-12)
+        if constexpr (G3D) { ARTES_CONSIDER(d_tout, 4, 1.e-12) ARTES_CONSIDER(d_pout, 5, 1.e-12) }
+    }
+#undef ARTES_CONSIDER
+    o.d = best;
+    o.ncr = cr; o.nct = ct; o.ncp = cp;
+    o.err = false;
+    switch (which) {
+        case 0: o.nft = 1; o.nfi = cr; o.ncr = cr - 1; break;
+        case 3: o.nft = 1; o.nfi = cr + 1; o.ncr = cr + 1; break;
+        case 1: o.nft = 2; o.nfi = ct; o.nct = ct - 1; break;
+        case 4: o.nft = 2; o.nfi = ct + 1; o.nct = ct + 1; break;
+        case 2: o.nft = 3; o.nfi = cp; o.ncp = (cp == 0) ? G.nphi - 1 : cp - 1; break;
+        case 5: o.nft = 3; o.nfi = pout; o.ncp = pout; break;
+        default: o.nft = 0; o.nfi = -999; o.err = true; log_err(R, 31); break;
+    }
+    o.exit = (o.nft == 1 && o.nfi == G.nr);
+    if (ft == 1 && fi == G.cell_depth && o.nft == 1 && o.nfi == G.cell_depth) { o.err = true; log_err(R, 34); }
+    if (o.ncr < 0) o.ncr = 0;
+}
+
+// ---------------------------------------------------- scattering physics ---
+// mueller_matrix_filler (ARTES.f90:1934-1960): returns c2p, s2p
+__device__ __forceinline__ void mueller(double psi, double& c2p, double& s2p) {
+    c2p = cos_b(2.0 * psi);
+    s2p = sqrt(1.0 - c2p * c2p);
+    if ((psi > HALF_PI && psi < PI) || (psi > 1.5 * PI && psi < TWO_PI) || (psi > -HALF_PI && psi < 0.0) ||
+        (psi > -TWO_PI && psi < -1.5 * PI))
+        s2p = -s2p;
+}
+
+// polarization_rotation (ARTES.f90:1663-1932); sc is scatter(4,4) row-major
+__device__ void polarization_rotation(const DevRun& R, double alpha, double beta, const double si[4],
+                                      const double sc[16], double d2, double dn2, double so[4], bool peeling) {
+    if (fabs(alpha) < 1.0 && fabs(dn2) < 1.0) {
+        double beta2 = 0.0;
+        const double num = (d2 - dn2 * alpha) / (sqrt(1.0 - alpha * alpha) * sqrt(1.0 - dn2 * dn2));
+        if (fabs(num) <= 1.0) beta2 = acos(num);
+        else if (num > 1.0 && num < 1.00001) beta2 = 0.0;
+        else if (num < -1.0 && num > -1.00001) beta2 = PI;
+        else log_err(R, 11);
+        double c, s;
+        mueller(beta, c, s);
+        double r0 = si[0], r1 = c * si[1] + s * si[2], r2 = -s * si[1] + c * si[2], r3 = si[3];
+        const double pr = sqrt(r1 * r1 + r2 * r2 + r3 * r3);
+        double norm = (pr > 0.0) ? sqrt(si[1] * si[1] + si[2] * si[2] + si[3] * si[3]) / pr : 1.0;
+        if (norm < 1.0 || norm > 1.0) { r1 *= norm; r2 *= norm; r3 *= norm; }
+        double q[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) q[i] = sc[i * 4 + 0] * r0 + sc[i * 4 + 1] * r1 + sc[i * 4 + 2] * r2 + sc[i * 4 + 3] * r3;
+        if (!peeling) {
+            if (q[0] > 0.0) {
+                norm = r0 / q[0];
+#pragma unroll
+                for (int i = 0; i < 4; i++) q[i] *= norm;
+            } else {
+                log_err(R, 12);
+            }
+        }
+        if (beta >= 0.0 && beta < PI) mueller(beta2, c, s);
+        else if (beta >= PI && beta < TWO_PI) mueller(-beta2, c, s);
+        so[0] = q[0];
+        so[1] = c * q[1] + s * q[2];
+        so[2] = -s * q[1] + c * q[2];
+        so[3] = q[3];
+        const double po = sqrt(so[1] * so[1] + so[2] * so[2] + so[3] * so[3]);
+        norm = (po > 0.0) ? sqrt(q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) / po : 1.0;
+        if (norm < 1.0 || norm > 1.0) { so[1] *= norm; so[2] *= norm; so[3] *= norm; }
+    } else if (alpha >= 1.0 && alpha < 1.0001) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) so[i] = si[i];
+        log_err(R, 13);
+    } else if (alpha <= -1.0 && alpha > -1.0001) {
+        double q[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) q[i] = sc[i * 4 + 0] * si[0] + sc[i * 4 + 1] * si[1] + sc[i * 4 + 2] * si[2] + sc[i * 4 + 3] * si[3];
+        if (peeling) {
+            for (int i = 0; i < 4; i++) so[i] = q[i];
+        } else if (q[0] > 0.0) {
+            const double norm = si[0] / q[0];
+            for (int i = 0; i < 4; i++) so[i] = norm * q[i];
+        } else {
+            for (int i = 0; i < 4; i++) so[i] = 0.0;
+            log_err(R, 14);
+        }
+        log_err(R, 15);
+    } else {
+        for (int i = 0; i < 4; i++) so[i] = si[i];
+        log_err(R, 16);
+    }
+}
+
+// direction_cosine (ARTES.f90:1962-2052)
+__device__ void direction_cosine(const DevRun& R, double alpha, double beta, double d0, double d1, double d2,
+                                 double& e0, double& e1, double& e2) {
+    const double cto = d2 / sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    const double sto = sqrt(1.0 - cto * cto);
+    double phi_old = atan2(d1, d0);
+    if (phi_old < 0.0) phi_old += TWO_PI;
+    double ctn = 0.0, phi_new = 0.0, spn = 0.0;
+    const bool upper = (beta >= PI && beta < TWO_PI);
+    const bool lower = (beta >= 0.0 && beta < PI);
+    if (upper) ctn = cto * alpha + sto * sqrt(1.0 - alpha * alpha) * cos_b(TWO_PI - beta);
+    else if (lower) ctn = cto * alpha + sto * sqrt(1.0 - alpha * alpha) * cos_b(beta);
+    else log_err(R, 18);
+    const double stn = sqrt(1.0 - ctn * ctn);
+    double num = (alpha - ctn * cto) / (stn * sto);
+    if (num >= 1.0) num = 1.0 - 1.e-10;
+    else if (num <= -1.0) num = -1.0 + 1.e-10;
+    if (fabs(num) <= 1.0) {
+        if (upper) phi_new = phi_old - acos(num);
+        else if (lower) phi_new = phi_old + acos(num);
+        else log_err(R, 19);
+    } else {
+        log_err(R, 20);
+    }
+    if (phi_new < 0.0) phi_new += TWO_PI;
+    if (phi_new > TWO_PI) phi_new -= TWO_PI;
+    const double cpn = cos_b(phi_new);
+    if (phi_new >= 0.0 && phi_new < PI) spn = sqrt(1.0 - cpn * cpn);
+    else if (phi_new >= PI && phi_new <= TWO_PI) spn = -sqrt(1.0 - cpn * cpn);
+    else log_err(R, 21);
+    e0 = stn * cpn;
+    e1 = stn * spn;
+    e2 = ctn;
+}
+
+// linear interpolation of the 16 elements at angle acos(mu) between bin centres
+// (ARTES.f90:1448-1530, 4780-4862); P = [180][16] of the cell's matrix
+__device__ __forceinline__ void interp_matrix(const double* __restrict__ P, double acos_mu, double sc[16]) {
+    const double deg = acos_mu * 180.0 / PI;
+    const int ideg = (int)deg;
+    int up, lo;
+    if (deg - (double)ideg > 0.5) { up = ideg + 2; lo = ideg + 1; }
+    else { up = ideg + 1; lo = ideg; }
+    if (up == 1) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) sc[i] = P[i];
+    } else if (lo == 180) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) sc[i] = P[179 * 16 + i];
+    } else {
+        const double* x0 = P + (lo - 1) * 16;
+        const double* x1 = P + (up - 1) * 16;
+        const double y0 = (double)lo - 0.5, y1 = (double)up - 0.5;
+        const double f = (deg - y0) / (y1 - y0);
+#pragma unroll
+        for (int i = 0; i < 16; i++) sc[i] = (x1[i] - x0[i]) * f + x0[i];
+    }
+}
+
+// smallest i in [1,180] with C(i) >= s for a non-decreasing C given by `cdf(i)`
+template <typename F>
+__device__ __forceinline__ int cdf_search(double s, F cdf) {
+    int lo = 1, hi = 180;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cdf(mid) >= s) hi = mid;
+            else lo = mid + 1;
+        }
+    }
+    return lo;
+}
+
+// scattering_angle_sampling (ARTES.f90:1534-1661) by binary search on the cumulative tables
+__device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* __restrict__ C, Rng& rng,
+                              const double st[4], double& alpha, double& beta) {
+    // azimuth: C_b(i) = i (p11 I + p14 V) + (p12 Q + p13 U) SC2(i) + (p12 U - p13 Q) SS2(i)
+    const double p11 = C[180 * 4 + 0], p12 = C[180 * 4 + 1], p13 = C[180 * 4 + 2], p14 = C[180 * 4 + 3];
+    const double u = p11 * st[0] + p14 * st[3];
+    const double v = p12 * st[1] + p13 * st[2];
+    const double w = p12 * st[2] - p13 * st[1];
+    auto cb = [&](int i) { return (double)i * u + v * G.sc2[i] + w * G.ss2[i]; };
+    double s = rng.uni() * cb(180);
+    int i = cdf_search(s, cb);
+    double y0 = cb(i - 1), y1 = cb(i);
+    beta = (s - y0) / (y1 - y0) + (double)(i - 1);
+    beta = beta * PI / 180.0;
+    if (rng.uni() > 0.5) beta = beta + PI;
+    if (beta >= TWO_PI) beta = TWO_PI - 1.e-10;
+    if (beta <= 0.0) beta = -TWO_PI + 1.e-10;
+    double c2b, s2b;
+    mueller(beta, c2b, s2b);
+    // polar: C_t(i) = I A1(i) + (c2b Q + s2b U) A2(i) + (c2b U - s2b Q) A3(i) + V A4(i)
+    const double k0 = st[0], k1 = c2b * st[1] + s2b * st[2], k2 = c2b * st[2] - s2b * st[1], k3 = st[3];
+    auto ct = [&](int j) {
+        const double* a = C + j * 4;
+        return k0 * a[0] + k1 * a[1] + k2 * a[2] + k3 * a[3];
+    };
+    s = rng.uni() * ct(180);
+    i = cdf_search(s, ct);
+    y0 = ct(i - 1);
+    y1 = ct(i);
+    const double adeg = (s - y0) / (y1 - y0) + (double)(i - 1);
+    alpha = cos_b(adeg * PI / 180.0);
+    if (fabs(alpha) >= 1.0) log_err(R, 56);
+    if (alpha >= 1.0) alpha = 1.0 - 1.e-10;
+    if (alpha <= -1.0) alpha = -1.0 + 1.e-10;
+}
+
+// ------------------------------------------------------------ the kernel ---
+enum Mode : int { M_NEW = 0, M_FIRST, M_PROP, M_PEEL, M_EV_FIRST, M_EV_INTERACT, M_EV_PEEL, M_DONE };
+enum End : int { E_NONE = -1, E_EXIT = 1, E_ABSORBED = 2, E_DROPPED = 3 };
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+
+}  // namespace artes

@@ -1,0 +1,577 @@
+// kernel_event.hpp -- the event-based engine ("event", default).
+//
+// The reference runs one packet per OpenMP thread from emission to exit
+// (ARTES.f90:546-955).  On a 64-lane wave that history-based form makes every wave
+// execute the union of all lanes' branches, and carrying the whole packet state plus
+// the scattering math in one kernel costs ~300 VGPRs (one wave per SIMD).  Here the
+// packet life is split at its natural seams into three kernels over a pool of P
+// in-flight packets whose state lives in HBM (SoA, ~250 B/packet):
+//
+//   k_trace  the hot loop: cell_face steps (ARTES.f90:2800-3470) of every trace --
+//            first optical depth (625-656), propagation (689-778, 848-941) and peel-off
+//            (4739-4761) -- plus the cheap transitions between them done inline:
+//            forced first interaction (660-685) and the scattering-loop head (793-813:
+//            roulette, albedo weight, minimum weight).  Lanes refill themselves from the
+//            trace list (wave-level grabs on 8 sharded cursors), so lanes stay busy until
+//            the list drains.  A segment ends when a peel-off trace ends (-> event list)
+//            or the packet ends (-> emit list).
+//   k_event  peel-off contribution (4765-4984) + scatter_photon / polarization_rotation
+//            (819-846) + the next optical depth; -> trace list.  All lanes run the same
+//            branchy math, so nothing is wasted on divergence.
+//   k_emit   closes finished packets (per-packet moments, counters, trace records) and
+//            emits new packets into the freed slots (emit_photon, 1027-1115) -> trace list.
+//
+// One host-side iteration = k_trace, k_event, k_emit, k_rotate; iterations repeat until
+// the trace list is empty.
+#pragma once
+
+#include "device_common.hpp"
+
+namespace artes {
+
+// packet-state pool (structure of arrays, P slots)
+struct Pool {
+    int P;
+    double *px, *py, *pz, *dx, *dy, *dz, *s0, *s1, *s2, *s3;
+    double *tx, *ty, *tz, *tacc, *ttgt;
+    double *cs0, *cs1, *cs2, *cs3, *pt0, *pt1, *pt2, *pt3, *peel_sum;
+    unsigned long long *r0, *r1, *pid;
+    int *pcell, *pface, *tcell, *tface, *mode, *cur_pix, *nscat, *ncross;
+};
+
+struct Lists {
+    const int* trace_in;  const int* trace_in_n;
+    int* trace_out;       int* trace_out_n;
+    int* event;           int* event_n;
+    int* emit;            int* emit_n;
+    unsigned int* grab;                 // [8] shard cursors of trace_in
+    unsigned long long* next_pkt;       // packets handed out so far
+};
+
+// slot modes
+enum SlotMode : int {
+    S_FRESH = 0,        // never held a packet
+    S_FIRST = 1, S_PROP = 2, S_PEEL = 3,       // trace kinds (in a trace list)
+    S_PEEL_DONE = 4,    // in the event list; bit 8 = exit, bit 9 = cell error
+    S_END_EXIT = 5, S_END_ABS = 6, S_END_DROP = 7,   // in the emit list
+    S_RETIRED = 8,
+};
+constexpr int FLAG_EXIT = 1 << 8;
+constexpr int FLAG_ERR = 1 << 9;
+
+__device__ __forceinline__ int pack_cell(int r, int t, int p) { return r | (t << 12) | (p << 22); }
+__device__ __forceinline__ void unpack_cell(int c, int& r, int& t, int& p) { r = c & 0xFFF; t = (c >> 12) & 0x3FF; p = (c >> 22) & 0x3FF; }
+__device__ __forceinline__ int pack_face(int type, int idx) { return (type << 28) | (idx & 0x0FFFFFFF); }
+__device__ __forceinline__ void unpack_face(int f, int& type, int& idx) { type = (f >> 28) & 0xF; idx = f & 0x0FFFFFFF; if (idx == 0x0FFFFFFF) idx = -1; }
+
+// wave-cooperative grab of up to popc(need) entries of a list split in 8 shards
+// (shard s = [s*n/8, (s+1)*n/8)); returns this lane's list index or -1
+__device__ __forceinline__ int wave_grab(unsigned int* cursors, int n, int home, bool need, bool& exhausted) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long mask = __ballot(need);
+    const int k = __popcll(mask);
+    const int rank = __popcll(mask & ((1ULL << lane) - 1ULL));
+    int got = 0, mine = -1;
+    for (int a = 0; a < 8 && got < k; a++) {
+        const int sh = (home + a) & 7;
+        const int lo = (int)(((long long)n * sh) >> 3), hi = (int)(((long long)n * (sh + 1)) >> 3);
+        const int want = k - got;
+        unsigned int base = 0;
+        if (lane == 0) base = atomicAdd(&cursors[sh], (unsigned int)want);
+        base = __shfl(base, 0);
+        const long long start = (long long)lo + base;
+        const int avail = (int)max(0LL, min((long long)want, (long long)hi - start));
+        if (need && rank >= got && rank < got + avail) mine = (int)start + (rank - got);
+        got += avail;
+    }
+    if (got == 0 && k > 0) exhausted = true;
+    return mine;
+}
+
+// Wave-aggregated append of this lane's `val` (if `want`) to a global list: one atomic
+// per wave instead of one per lane.  Same-address device-scope atomics are serialised
+// at the memory side (the L2s of the 8 XCDs are not coherent), so per-lane appends to
+// the list counters would cost ~10 ns per packet event.
+__device__ __forceinline__ void wave_append(bool want, int val, int* list, int* list_n) {
+    const unsigned long long mask = __ballot(want);
+    if (mask == 0) return;
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == __ffsll((long long)mask) - 1) base = atomicAdd(list_n, __popcll(mask));
+    base = __shfl(base, __ffsll((long long)mask) - 1);
+    if (want) list[base + __popcll(mask & ((1ULL << lane) - 1ULL))] = val;
+}
+
+// Per-wave LDS staging queue (64 entries) in front of a global list, for producers whose
+// lanes finish at scattered times (k_trace): flushed with one atomic per 64 entries.
+struct WaveQueue {
+    int* buf;     // this wave's 64 LDS entries
+    int cnt;      // wave-uniform fill level
+    __device__ __forceinline__ void flush(int* list, int* list_n) {
+        if (cnt == 0) return;
+        const int lane = threadIdx.x & 63;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(list_n, cnt);
+        base = __shfl(base, 0);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < cnt) list[base + lane] = buf[lane];
+        __builtin_amdgcn_wave_barrier();
+        cnt = 0;
+    }
+    __device__ __forceinline__ void push(bool want, int val, int* list, int* list_n) {
+        const unsigned long long mask = __ballot(want);
+        const int k = __popcll(mask);
+        if (k == 0) return;
+        if (cnt + k > 64) flush(list, list_n);
+        const int lane = threadIdx.x & 63;
+        if (want) buf[cnt + __popcll(mask & ((1ULL << lane) - 1ULL))] = val;
+        __builtin_amdgcn_wave_barrier();
+        cnt += k;
+    }
+};
+
+template <bool G3D>
+__global__ __launch_bounds__(BLOCK) void k_trace(DevGrid G, DevRun R, Pool S, Lists L) {
+    const int n = *L.trace_in_n;
+    const int home = blockIdx.x & 7;
+    __shared__ int s_q[2][BLOCK];
+    const int wbase = threadIdx.x & ~63;
+    WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
+    bool exhausted = false, have = false;
+    int slot = -1, mode = 0, tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0;
+    double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, ttgt = 0;
+    uint32_t c_cross = 0, c_peel = 0, seg_cross = 0;
+
+    for (;;) {
+        // ---------------------------------------------------------------- refill
+        if (!exhausted) {
+            const unsigned long long idle = __ballot(!have);
+            if (__popcll(idle) >= 32 || idle == __ballot(true)) {
+                const int my = wave_grab(L.grab, n, home, !have, exhausted);
+                if (!have && my >= 0) {
+                    slot = L.trace_in[my];
+                    mode = S.mode[slot];
+                    tx = S.tx[slot]; ty = S.ty[slot]; tz = S.tz[slot];
+                    tacc = S.tacc[slot]; ttgt = S.ttgt[slot];
+                    unpack_cell(S.tcell[slot], tcr, tct, tcp);
+                    unpack_face(S.tface[slot], tft, tfi);
+                    if (mode == S_PEEL) { nx = R.det0; ny = R.det1; nz = R.det2; }
+                    else { nx = S.dx[slot]; ny = S.dy[slot]; nz = S.dz[slot]; }
+                    seg_cross = 0;
+                    have = true;
+                }
+            }
+        }
+        if (!__any(have)) break;
+        int end = 0;   // 0: continue, else the slot's new mode
+        if (have) {
+        // ------------------------------------------------------------ trace step
+        Step o;
+        cell_face<G3D>(G, R, tx, ty, tz, nx, ny, nz, tft, tfi, tcr, tct, tcp, o);
+        c_cross++;
+        seg_cross++;
+        const double k = G.kappa[tcr + G.nr * (tct + G.ntheta * tcp)];
+        const double tau_cell = o.d * k;
+        const bool surf = (o.nft == 1 && o.nfi == G.cell_depth);
+        if (mode == S_PROP) {
+            if (o.err) {
+                log_err(R, 3);
+                end = S_END_DROP;
+            } else if (tacc + tau_cell > ttgt) {          // interaction in this cell (ARTES.f90:705-720)
+                const double s = (ttgt - tacc) / k;
+                const double px = tx + s * nx, py = ty + s * ny, pz = tz + s * nz;
+                S.px[slot] = px; S.py[slot] = py; S.pz[slot] = pz;
+                S.pcell[slot] = pack_cell(tcr, tct, tcp);
+                S.pface[slot] = 0;
+                // scattering-loop head (ARTES.f90:788-813)
+                Rng rng; rng.s0 = S.r0[slot]; rng.s1 = S.r1[slot];
+                bool stop = !R.photon_scattering;
+                if (!stop) stop = rng.uni() < R.fstop;
+                if (!stop) {
+                    const double alb = G.albedo[tcr + G.nr * (tct + G.ntheta * tcp)];
+                    if (alb < 1.0 && alb > 0.0) {
+                        const double gamma = alb / (1.0 - R.fstop);
+                        S.s0[slot] *= gamma; S.s1[slot] *= gamma; S.s2[slot] *= gamma; S.s3[slot] *= gamma;
+                    }
+                    if (S.s0[slot] <= R.pmin) stop = true;
+                }
+                S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+                if (stop) {
+                    end = S_END_ABS;
+                } else {                                   // peel-off trace (ARTES.f90:4722-4761)
+                    c_peel++;
+                    tx = px; ty = py; tz = pz;
+                    nx = R.det0; ny = R.det1; nz = R.det2;
+                    tft = 0; tfi = 0;
+                    tacc = 0.0;
+                    mode = S_PEEL;
+                }
+            } else {
+                tx += o.d * nx; ty += o.d * ny; tz += o.d * nz;
+                tft = o.nft; tfi = o.nfi; tcr = o.ncr; tct = o.nct; tcp = o.ncp;
+                if (o.exit) {
+                    end = S_END_EXIT;
+                } else if (surf) {
+                    Rng rng; rng.s0 = S.r0[slot]; rng.s1 = S.r1[slot];
+                    const double xi = rng.uni();
+                    S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+                    if (xi > R.surface_albedo) end = S_END_ABS;
+                    else { log_err(R, 62); end = S_END_DROP; }
+                } else {
+                    tacc += tau_cell;
+                }
+            }
+        } else {   // S_FIRST or S_PEEL: accumulate optical depth to the boundary
+            tacc += tau_cell;
+            tx += o.d * nx; ty += o.d * ny; tz += o.d * nz;
+            if (o.err) log_err(R, mode == S_FIRST ? 2 : 43);
+            if (o.exit || o.err || surf) {
+                if (mode == S_PEEL) {
+                    S.tacc[slot] = tacc;
+                    end = S_PEEL_DONE | (o.exit ? FLAG_EXIT : 0) | (o.err ? FLAG_ERR : 0);
+                } else {   // forced first interaction (ARTES.f90:658-685)
+                    const double tau_first = tacc;
+                    if (tau_first < 1.e-6 && !surf) {
+                        end = S_END_DROP;
+                    } else {
+                        Rng rng; rng.s0 = S.r0[slot]; rng.s1 = S.r1[slot];
+                        const double xi = rng.uni();
+                        double tau;
+                        if (tau_first < 1.e-6) {
+                            tau = -log(1.0 - xi);
+                        } else if (tau_first < 50.0) {
+                            const double e = 1.0 - exp(-tau_first);
+                            tau = -log(1.0 - xi * e);
+                            S.s0[slot] *= e; S.s1[slot] *= e; S.s2[slot] *= e; S.s3[slot] *= e;
+                        } else {
+                            tau = -log(1.0 - xi);
+                        }
+                        S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+                        tx = S.px[slot]; ty = S.py[slot]; tz = S.pz[slot];
+                        unpack_cell(S.pcell[slot], tcr, tct, tcp);
+                        unpack_face(S.pface[slot], tft, tfi);
+                        tacc = 0.0; ttgt = tau;
+                        mode = S_PROP;
+                    }
+                }
+            } else {
+                tft = o.nft; tfi = o.nfi; tcr = o.ncr; tct = o.nct; tcp = o.ncp;
+            }
+        }
+        if (end) {
+            S.mode[slot] = end;
+            S.ncross[slot] += seg_cross;
+            have = false;
+        }
+        }   // have
+        q_event.push(end && (end & 0xFF) == S_PEEL_DONE, slot, L.event, L.event_n);
+        q_emit.push(end && (end & 0xFF) != S_PEEL_DONE, slot, L.emit, L.emit_n);
+    }
+    q_event.flush(L.event, L.event_n);
+    q_emit.flush(L.emit, L.emit_n);
+    const unsigned long long w = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);
+    if ((threadIdx.x & 63) == 0) {
+        if (w) atomicAdd(&R.cnt[ARTES_CNT_CROSSINGS], w);
+        if (wp) atomicAdd(&R.cnt[ARTES_CNT_PEELS], wp);
+    }
+}
+
+// park the packet in a new propagation trace starting at its position
+__device__ __forceinline__ void start_prop(const Pool& S, int slot, double tau) {
+    S.tx[slot] = S.px[slot]; S.ty[slot] = S.py[slot]; S.tz[slot] = S.pz[slot];
+    S.tcell[slot] = S.pcell[slot];
+    S.tface[slot] = S.pface[slot];
+    S.tacc[slot] = 0.0;
+    S.ttgt[slot] = tau;
+    S.mode[slot] = S_PROP;
+}
+
+// one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended)
+__device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
+                                         size_t plane, uint32_t& c_scat, uint32_t& c_det) {
+    {
+        const int m = S.mode[slot];
+        if (m & FLAG_ERR) { S.mode[slot] = S_END_DROP; return 2; }
+        const double px = S.px[slot], py = S.py[slot], pz = S.pz[slot];
+        double dx = S.dx[slot], dy = S.dy[slot], dz = S.dz[slot];
+        double st[4] = {S.s0[slot], S.s1[slot], S.s2[slot], S.s3[slot]};
+        int cr, ct, cp;
+        unpack_cell(S.pcell[slot], cr, ct, cp);
+        const int cell = cr + G.nr * (ct + G.ntheta * cp);
+        const int mid = G.matid[cell];
+        const double* __restrict__ P = G.mats + (size_t)mid * MAT_DOUBLES;
+        const double tau_peel = S.tacc[slot];
+        bool drop = false;
+        if ((m & FLAG_EXIT) && tau_peel < 50.0) {
+            const double w = exp(-tau_peel);
+            double mu = dx * R.det0 + dy * R.det1 + dz * R.det2;
+            if (mu >= 1.0) mu = 1.0 - 1.e-10;
+            else if (mu <= -1.0) mu = -1.0 + 1.e-10;
+            double sc[16];
+            interp_matrix(P, acos(mu), sc);
+            double phi_old = atan2(dy, dx);
+            if (phi_old < 0.0) phi_old += TWO_PI;
+            if (phi_old > TWO_PI) phi_old -= TWO_PI;
+            double phi_new = atan2(R.det1, R.det0);
+            if (phi_new < 0.0) phi_new += TWO_PI;
+            if (phi_new > TWO_PI) phi_new -= TWO_PI;
+            bool have_out = false;
+            double so[4] = {0, 0, 0, 0};
+            if (fabs(dz) < 1.0) {
+                const double num = (R.det2 - dz * mu) / (sqrt(1.0 - mu * mu) * sqrt(1.0 - dz * dz));
+                double phs = 0.0;
+                if (fabs(num) < 1.0) phs = acos(num);
+                else if (num >= 1.0) phs = 1.e-10;
+                else if (num <= -1.0) phs = PI - 1.e-10;
+                else log_err(R, 44);
+                if (phi_old - phi_new >= 0.0 && phi_old - phi_new < PI) phs = TWO_PI - phs;
+                if (TWO_PI + phi_old - phi_new >= 0.0 && TWO_PI + phi_old - phi_new < PI) phs = TWO_PI - phs;
+                if (phs < 0.0) phs += TWO_PI;
+                if (fabs(mu) < 1.0) {
+                    polarization_rotation(R, mu, phs, st, sc, dz, R.det2, so, true);
+                    have_out = true;
+                } else {
+                    log_err(R, 49);
+                    drop = true;
+                }
+            } else {
+                log_err(R, 45);
+            }
+            if (have_out && !drop) {
+                const double x_im = py * R.cdp - px * R.sdp;
+                const double y_im = pz * R.sdt - py * R.cdt * R.sdp - px * R.cdt * R.cdp;
+                const int ix = (int)((double)R.nx * (x_im + R.x_max) / (2.0 * R.x_max));
+                const int iy = (int)((double)R.ny * (y_im + R.y_max) / (2.0 * R.y_max));
+                const double wI = w * so[0];
+                if (wI > 0.0 && wI < 1.e100) {
+                    if (ix < 0 || ix >= R.nx || iy < 0 || iy >= R.ny) {
+                        log_err(R, 63);
+                    } else {
+                        const int pix = iy * R.nx + ix;
+                        const double v[4] = {w * so[0], -w * so[1], w * so[2], w * so[3]};   // -Q: ARTES.f90:4956
+                        const int cur = S.cur_pix[slot];
+                        double cs[4] = {S.cs0[slot], S.cs1[slot], S.cs2[slot], S.cs3[slot]};
+                        if (pix != cur) {
+                            if (cur >= 0) {
+#pragma unroll
+                                for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
+                            }
+                            S.cur_pix[slot] = pix;
+                            cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            unsafeAtomicAdd(&det[q * plane + pix], v[q]);
+                            unsafeAtomicAdd(&det[(4 + q) * plane + pix], v[q] * v[q]);
+                            cs[q] += v[q];
+                        }
+                        unsafeAtomicAdd(&det[8 * plane + pix], 1.0);
+                        S.cs0[slot] = cs[0]; S.cs1[slot] = cs[1]; S.cs2[slot] = cs[2]; S.cs3[slot] = cs[3];
+                        S.pt0[slot] += v[0]; S.pt1[slot] += v[1]; S.pt2[slot] += v[2]; S.pt3[slot] += v[3];
+                        S.peel_sum[slot] += wI;
+                        c_det++;
+                    }
+                } else {
+                    log_err(R, 53);
+                }
+            }
+        }
+        if (drop) { S.mode[slot] = S_END_DROP; return 2; }
+        // scatter_photon + polarization_rotation (ARTES.f90:819-846)
+        c_scat++;
+        S.nscat[slot] += 1;
+        Rng rng; rng.s0 = S.r0[slot]; rng.s1 = S.r1[slot];
+        double alpha, beta;
+        sample_angles(G, R, G.cums + (size_t)mid * CUM_DOUBLES, rng, st, alpha, beta);
+        double e0, e1, e2;
+        direction_cosine(R, alpha, beta, dx, dy, dz, e0, e1, e2);
+        double sc[16];
+        interp_matrix(P, acos(alpha), sc);
+        if (fabs(alpha) < 1.0) {
+            double sn[4];
+            polarization_rotation(R, alpha, beta, st, sc, dz, e2, sn, false);
+            S.s0[slot] = sn[0]; S.s1[slot] = sn[1]; S.s2[slot] = sn[2]; S.s3[slot] = sn[3];
+            S.dx[slot] = e0; S.dy[slot] = e1; S.dz[slot] = e2;
+            const double xi = rng.uni();
+            S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+            start_prop(S, slot, -log(1.0 - xi));
+            return 1;
+        } else {
+            log_err(R, 50);
+            S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+            S.mode[slot] = S_END_DROP;
+            return 2;
+        }
+    }
+}
+
+// peel-off contribution + scattering (ARTES.f90:4765-4984, 819-846)
+__global__ __launch_bounds__(BLOCK) void k_event(DevGrid G, DevRun R, Pool S, Lists L) {
+    const int n = *L.event_n;
+    const size_t plane = (size_t)R.nx * R.ny;
+    double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
+    uint32_t c_scat = 0, c_det = 0;
+    const int n_pad = (n + 63) & ~63;   // whole waves iterate together (wave-aggregated appends)
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
+        const int slot = i < n ? L.event[i] : -1;
+        const int dest = slot >= 0 ? event_one(G, R, S, slot, det, plane, c_scat, c_det) : 0;
+        wave_append(dest == 1, slot, L.trace_out, L.trace_out_n);
+        wave_append(dest == 2, slot, L.emit, L.emit_n);
+    }
+    const unsigned long long ws = wave_sum_u64(c_scat), wd = wave_sum_u64(c_det);
+    if ((threadIdx.x & 63) == 0) {
+        if (ws) atomicAdd(&R.cnt[ARTES_CNT_SCATTERS], ws);
+        if (wd) atomicAdd(&R.cnt[ARTES_CNT_DETECTED], wd);
+    }
+}
+
+// close finished packets and emit new ones (ARTES.f90:546-597, 1027-1115, 2605-2669)
+template <bool G3D, bool TRACE>
+__global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lists L) {
+    const int n = *L.emit_n;
+    const size_t plane = (size_t)R.nx * R.ny;
+    double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
+    uint32_t c_exit = 0, c_abs = 0, c_drop = 0, c_pkt = 0;
+    double t2[4] = {0, 0, 0, 0};
+    const int n_pad = (n + 63) & ~63;
+    const int lane = threadIdx.x & 63;
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
+        const int slot = i < n ? L.emit[i] : -1;
+        const int m = slot >= 0 ? S.mode[slot] : S_RETIRED;
+        if (m == S_END_EXIT || m == S_END_ABS || m == S_END_DROP) {
+            if (m == S_END_EXIT) c_exit++;
+            else if (m == S_END_ABS) c_abs++;
+            else c_drop++;
+            const int cur = S.cur_pix[slot];
+            if (cur >= 0) {
+                unsafeAtomicAdd(&det[12 * plane + cur], S.cs0[slot] * S.cs0[slot]);
+                unsafeAtomicAdd(&det[13 * plane + cur], S.cs1[slot] * S.cs1[slot]);
+                unsafeAtomicAdd(&det[14 * plane + cur], S.cs2[slot] * S.cs2[slot]);
+                unsafeAtomicAdd(&det[15 * plane + cur], S.cs3[slot] * S.cs3[slot]);
+            }
+            const double a0 = S.pt0[slot], a1 = S.pt1[slot], a2 = S.pt2[slot], a3 = S.pt3[slot];
+            t2[0] += a0 * a0; t2[1] += a1 * a1; t2[2] += a2 * a2; t2[3] += a3 * a3;
+            if constexpr (TRACE) {
+                double* rr = R.rec + (size_t)(S.pid[slot] - R.first) * 4;
+                rr[0] = S.peel_sum[slot];
+                rr[1] = (double)S.nscat[slot];
+                rr[2] = (double)S.ncross[slot];
+                rr[3] = (double)(m - S_END_EXIT + 1);   // 1 exit, 2 absorbed, 3 dropped
+            }
+        }
+        // packet ids for the lanes that need one: one atomic per wave
+        const bool need = (m != S_RETIRED);
+        const unsigned long long mask = __ballot(need);
+        unsigned long long k = 0;
+        if (mask) {
+            const int leader = __ffsll((long long)mask) - 1;
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(L.next_pkt, (unsigned long long)__popcll(mask));
+            base = __shfl(base, leader);
+            k = base + __popcll(mask & ((1ULL << lane) - 1ULL));
+        }
+        const bool emit = need && k < R.n;
+        if (need && !emit) S.mode[slot] = S_RETIRED;
+        if (emit) {
+        c_pkt++;
+        const unsigned long long pid = R.first + k;
+        Rng rng;
+        rng.seed(R.seed, pid);
+        // emit_photon, star branch (ARTES.f90:1027-1115)
+        const double Rt = G.rtop;
+        double r_disk, phi_disk;
+        if (R.phase_far) {
+            do { r_disk = sqrt(rng.uni()); } while (!(r_disk > 0.9));
+            phi_disk = TWO_PI * rng.uni();
+        } else {
+            r_disk = sqrt(rng.uni());
+            phi_disk = TWO_PI * rng.uni();
+        }
+        double sphi, cphi;
+        sincos_bounded(phi_disk, sphi, cphi);
+        const double d1 = Rt * r_disk * sphi, d2 = Rt * r_disk * cphi;
+        double dx = -1.0, dy = 0.0, dz = 0.0;
+        double px = sqrt(Rt * Rt - d1 * d1 - d2 * d2), py = d1, pz = d2;
+        if (R.stellar_direction) {   // ARTES.f90:1080-1111
+            double c = cos_b(-(HALF_PI - R.theta_star)), s = sin_b(-(HALF_PI - R.theta_star));
+            const double x1 = c * px + s * pz, y1 = py, z1 = -s * px + c * pz;
+            c = cos_b(R.phi_star); s = sin_b(R.phi_star);
+            px = c * x1 - s * y1; py = s * x1 + c * y1; pz = z1;
+            double td = PI - R.theta_star, pd = PI + R.phi_star;
+            if (td < 0.0) td += TWO_PI;
+            if (td > TWO_PI) td -= TWO_PI;
+            if (pd < 0.0) pd += TWO_PI;
+            if (pd > TWO_PI) pd -= TWO_PI;
+            dx = sin_b(td) * cos_b(pd); dy = sin_b(td) * sin_b(pd); dz = cos_b(td);
+        }
+        int cr = G.nr - 1, ct = 0, cp = 0;   // initial_cell (ARTES.f90:2605-2669)
+        if constexpr (G3D) {
+            const double r = sqrt(px * px + py * py + pz * pz);
+            const double th = acos(pz / r);
+            double ph = atan2(py, px);
+            if (ph < 0.0) ph += TWO_PI;
+            for (int j = 0; j < G.ntheta; j++)
+                if (th > G.thetaf[j] && th < G.thetaf[j + 1]) { ct = j; break; }
+            for (int j = 0; j < G.nphi; j++) {
+                const double hi = (j < G.nphi - 1) ? G.phif[j + 1] : TWO_PI;
+                if (ph > G.phif[j] && ph < hi) { cp = j; break; }
+            }
+        }
+        S.pid[slot] = pid;
+        S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+        S.px[slot] = px; S.py[slot] = py; S.pz[slot] = pz;
+        S.dx[slot] = dx; S.dy[slot] = dy; S.dz[slot] = dz;
+        S.s0[slot] = 1.0; S.s1[slot] = 0.0; S.s2[slot] = 0.0; S.s3[slot] = 0.0;
+        const int pc = pack_cell(cr, ct, cp), pf = pack_face(1, G.nr);
+        S.pcell[slot] = pc; S.pface[slot] = pf;
+        S.tx[slot] = px; S.ty[slot] = py; S.tz[slot] = pz;
+        S.tcell[slot] = pc; S.tface[slot] = pf;
+        S.tacc[slot] = 0.0; S.ttgt[slot] = 0.0;
+        S.cs0[slot] = S.cs1[slot] = S.cs2[slot] = S.cs3[slot] = 0.0;
+        S.pt0[slot] = S.pt1[slot] = S.pt2[slot] = S.pt3[slot] = 0.0;
+        S.peel_sum[slot] = 0.0;
+        S.cur_pix[slot] = -1;
+        S.nscat[slot] = 0;
+        S.ncross[slot] = 0;
+        S.mode[slot] = S_FIRST;
+        }   // emit
+        wave_append(emit, slot, L.trace_out, L.trace_out_n);
+    }
+    const unsigned long long a = wave_sum_u64(c_exit), b = wave_sum_u64(c_abs), c = wave_sum_u64(c_drop),
+                             d = wave_sum_u64(c_pkt);
+    const double q0 = wave_sum_f64(t2[0]), q1 = wave_sum_f64(t2[1]), q2 = wave_sum_f64(t2[2]), q3 = wave_sum_f64(t2[3]);
+    if ((threadIdx.x & 63) == 0) {
+        if (a) atomicAdd(&R.cnt[ARTES_CNT_EXITED], a);
+        if (b) atomicAdd(&R.cnt[ARTES_CNT_ABSORBED], b);
+        if (c) atomicAdd(&R.cnt[ARTES_CNT_DROPPED], c);
+        if (d) atomicAdd(&R.cnt[ARTES_CNT_PACKETS], d);
+        if (q0 != 0.0) unsafeAtomicAdd(&R.tot2[0], q0);
+        if (q1 != 0.0) unsafeAtomicAdd(&R.tot2[1], q1);
+        if (q2 != 0.0) unsafeAtomicAdd(&R.tot2[2], q2);
+        if (q3 != 0.0) unsafeAtomicAdd(&R.tot2[3], q3);
+    }
+}
+
+// initial fill: every slot is fresh and queued for emission
+__global__ void k_init(Pool S, int* emit, int* emit_n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S.P) {
+        S.mode[i] = S_FRESH;
+        emit[i] = i;
+    }
+    if (i == 0) *emit_n = S.P;
+}
+
+// end of an iteration: the output trace list becomes the input, the consumed input
+// buffer is reset to become the next output; event/emit lists and cursors are zeroed
+__global__ void k_rotate(int* in_n, int* out_n, int* event_n, int* emit_n, unsigned int* grab) {
+    if (threadIdx.x == 0) {
+        *in_n = 0;          // this buffer is the next iteration's output
+        (void)out_n;        // keeps its count: it is the next iteration's input
+        *event_n = 0;
+        *emit_n = 0;
+    }
+    if (threadIdx.x < 8) grab[threadIdx.x] = 0;
+}
+
+}  // namespace artes

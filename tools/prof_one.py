@@ -1,0 +1,18 @@
+"""One engine run for profiling: python tools/prof_one.py <config> <packets>."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from artes_amd import driver, synthetic  # noqa: E402
+from artes_amd.engine import Grid  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "ray3d"
+n = int(float(sys.argv[2])) if len(sys.argv) > 2 else 10**7
+cfg = driver.default_config()
+atm = synthetic.make_config(name, share_matrix=True)
+det = driver.detector_geometry(cfg, atm["radial"][-1])
+g = Grid(atm, 0)
+p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0))
+g.run(p, 0, 10**5, 1)
+r = g.run(p, 0, n, 2024)
+print(name, n, "kernel ms %.1f -> %.3g pkt/s" % (g.last_kernel_ms(), n / (g.last_kernel_ms() * 1e-3)), flush=True)
