@@ -41,7 +41,7 @@ struct DevGrid {
 
 struct DevRun {
     uint64_t first, n, seed;
-    int nx, ny, photon_scattering, phase_far, stellar_direction, defer;
+    int nx, ny, photon_scattering, phase_far, stellar_direction, defer, refill, static_q64;
     double det0, det1, det2, sdt, cdt, sdp, cdp;
     double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
     double* __restrict__ det;       // [NCOPY][4][4][ny][nx]

@@ -29,14 +29,33 @@
 
 namespace artes {
 
-// packet-state pool (structure of arrays, P slots)
+// packet-state pool: one 256-byte record per slot (two 128-byte cache lines).  The
+// work lists visit slots in no particular order, so a record layout keeps every access
+// of a lane inside its own two lines; a structure-of-arrays pool would touch one line per
+// field per lane.  Line 0 holds what k_trace needs, line 1 the event-only state.
+struct alignas(256) Slot {
+    // line 0: trace state
+    double tx, ty, tz, tacc, ttgt;      // trace position, accumulated / target optical depth
+    double dx, dy, dz;                  // packet direction
+    int tcell, tface;                   // trace cell / entry face (packed)
+    int mode, ncross;
+    unsigned long long r0, r1;          // xoroshiro128++ state
+    double px, py, pz;                  // packet position (last interaction / emission)
+    int pcell, pface;
+    // line 1: event state
+    double s0, s1, s2, s3;              // Stokes vector
+    double cs0, cs1, cs2, cs3;          // running contribution to the current pixel
+    double pt0, pt1, pt2, pt3;          // packet total per Stokes
+    double peel_sum;                    // trace records: total peeled intensity
+    unsigned long long pid;
+    int cur_pix, nscat;
+    double spare;
+};
+static_assert(sizeof(Slot) == 256, "slot record must be two cache lines");
+
 struct Pool {
     int P;
-    double *px, *py, *pz, *dx, *dy, *dz, *s0, *s1, *s2, *s3;
-    double *tx, *ty, *tz, *tacc, *ttgt;
-    double *cs0, *cs1, *cs2, *cs3, *pt0, *pt1, *pt2, *pt3, *peel_sum;
-    unsigned long long *r0, *r1, *pid;
-    int *pcell, *pface, *tcell, *tface, *mode, *cur_pix, *nscat, *ncross;
+    Slot* __restrict__ s;
 };
 
 struct Lists {
@@ -64,17 +83,48 @@ __device__ __forceinline__ void unpack_cell(int c, int& r, int& t, int& p) { r =
 __device__ __forceinline__ int pack_face(int type, int idx) { return (type << 28) | (idx & 0x0FFFFFFF); }
 __device__ __forceinline__ void unpack_face(int f, int& type, int& idx) { type = (f >> 28) & 0xF; idx = f & 0x0FFFFFFF; if (idx == 0x0FFFFFFF) idx = -1; }
 
-// wave-cooperative grab of up to popc(need) entries of a list split in 8 shards
-// (shard s = [s*n/8, (s+1)*n/8)); returns this lane's list index or -1
-__device__ __forceinline__ int wave_grab(unsigned int* cursors, int n, int home, bool need, bool& exhausted) {
+// Work distribution over the trace list: the first `n_static` entries are split into one
+// contiguous chunk per wave (no atomics: a wave-local cursor), the rest is grabbed
+// dynamically through 8 sharded cursors to balance the tail.  Device-scope atomics are
+// resolved at the memory side (~µs round trip), so a purely dynamic grab stalls every
+// refill; the static part keeps most refills at one list load + one record load.
+struct TraceCursor {
+    int pos, end;              // static chunk of this wave (wave-uniform)
+    int dyn_lo, dyn_n;         // dynamic range
+    bool exhausted;
+};
+
+__device__ __forceinline__ TraceCursor make_cursor(int n, int static_q64) {
+    const long long W = (long long)gridDim.x * (BLOCK / 64);
+    const long long w = (long long)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+    const int n_static = (int)(((long long)n * static_q64) >> 6);
+    TraceCursor c;
+    c.pos = (int)((n_static * w) / W);
+    c.end = (int)((n_static * (w + 1)) / W);
+    c.dyn_lo = n_static;
+    c.dyn_n = n - n_static;
+    c.exhausted = (n == 0);
+    return c;
+}
+
+// hand out up to popc(need) list indices to the lanes with `need`; returns this lane's or -1
+__device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, int home, bool need) {
     const int lane = threadIdx.x & 63;
     const unsigned long long mask = __ballot(need);
     const int k = __popcll(mask);
     const int rank = __popcll(mask & ((1ULL << lane) - 1ULL));
     int got = 0, mine = -1;
+    if (c.pos < c.end) {
+        got = min(k, c.end - c.pos);
+        if (need && rank < got) mine = c.pos + rank;
+        c.pos += got;
+        return mine;
+    }
     for (int a = 0; a < 8 && got < k; a++) {
         const int sh = (home + a) & 7;
-        const int lo = (int)(((long long)n * sh) >> 3), hi = (int)(((long long)n * (sh + 1)) >> 3);
+        const int lo = c.dyn_lo + (int)(((long long)c.dyn_n * sh) >> 3);
+        const int hi = c.dyn_lo + (int)(((long long)c.dyn_n * (sh + 1)) >> 3);
+        if (hi <= lo) continue;
         const int want = k - got;
         unsigned int base = 0;
         if (lane == 0) base = atomicAdd(&cursors[sh], (unsigned int)want);
@@ -84,7 +134,7 @@ __device__ __forceinline__ int wave_grab(unsigned int* cursors, int n, int home,
         if (need && rank >= got && rank < got + avail) mine = (int)start + (rank - got);
         got += avail;
     }
-    if (got == 0 && k > 0) exhausted = true;
+    if (got == 0 && k > 0) c.exhausted = true;
     return mine;
 }
 
@@ -130,33 +180,67 @@ struct WaveQueue {
     }
 };
 
-template <bool G3D>
-__global__ __launch_bounds__(BLOCK) void k_trace(DevGrid G, DevRun R, Pool S, Lists L) {
+// bytes of LDS holding the per-coordinate face tables (rf2, thetaf, tan2, phis, phic, tplane)
+__host__ __device__ inline size_t face_table_bytes(int nr, int ntheta, int nphi) {
+    return sizeof(double) * ((size_t)(nr + 1) + 2 * (size_t)(ntheta + 1) + 2 * (size_t)nphi) + sizeof(int) * (size_t)(ntheta + 1);
+}
+
+// stage the face tables in LDS: every trace step reads ~12 of them at indices that depend
+// on the previous step, so their latency is on the critical path; LDS answers in ~64
+// cycles where an L2 hit takes ~200-500
+__device__ __forceinline__ DevGrid stage_face_tables(const DevGrid& G, double* lds) {
+    DevGrid GL = G;
+    double* p = lds;
+    auto copy = [&](const double* src, int cnt) {
+        for (int i = threadIdx.x; i < cnt; i += BLOCK) p[i] = src[i];
+        double* out = p;
+        p += cnt;
+        return out;
+    };
+    GL.rf2 = copy(G.rf2, G.nr + 1);
+    GL.thetaf = copy(G.thetaf, G.ntheta + 1);
+    GL.tan2 = copy(G.tan2, G.ntheta + 1);
+    GL.phis = copy(G.phis, G.nphi);
+    GL.phic = copy(G.phic, G.nphi);
+    int* ip = (int*)p;
+    for (int i = threadIdx.x; i < G.ntheta + 1; i += BLOCK) ip[i] = G.tplane[i];
+    GL.tplane = ip;
+    __syncthreads();
+    return GL;
+}
+
+template <bool G3D, int WPE, bool LDS>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G0, DevRun R, Pool S, Lists L) {
+    extern __shared__ double s_tab[];
+    const DevGrid G = LDS ? stage_face_tables(G0, s_tab) : G0;
     const int n = *L.trace_in_n;
     const int home = blockIdx.x & 7;
     __shared__ int s_q[2][BLOCK];
     const int wbase = threadIdx.x & ~63;
     WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
-    bool exhausted = false, have = false;
+    TraceCursor cur = make_cursor(n, R.static_q64);
+    bool have = false;
     int slot = -1, mode = 0, tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0;
     double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, ttgt = 0;
     uint32_t c_cross = 0, c_peel = 0, seg_cross = 0;
 
     for (;;) {
         // ---------------------------------------------------------------- refill
-        if (!exhausted) {
+        if (!cur.exhausted) {
             const unsigned long long idle = __ballot(!have);
-            if (__popcll(idle) >= 32 || idle == __ballot(true)) {
-                const int my = wave_grab(L.grab, n, home, !have, exhausted);
+            if (__popcll(idle) >= R.refill || idle == __ballot(true)) {
+                const int my = wave_take(cur, L.grab, home, !have);
                 if (!have && my >= 0) {
                     slot = L.trace_in[my];
-                    mode = S.mode[slot];
-                    tx = S.tx[slot]; ty = S.ty[slot]; tz = S.tz[slot];
-                    tacc = S.tacc[slot]; ttgt = S.ttgt[slot];
-                    unpack_cell(S.tcell[slot], tcr, tct, tcp);
-                    unpack_face(S.tface[slot], tft, tfi);
-                    if (mode == S_PEEL) { nx = R.det0; ny = R.det1; nz = R.det2; }
-                    else { nx = S.dx[slot]; ny = S.dy[slot]; nz = S.dz[slot]; }
+                    mode = S.s[slot].mode;
+                    tx = S.s[slot].tx; ty = S.s[slot].ty; tz = S.s[slot].tz;
+                    tacc = S.s[slot].tacc; ttgt = S.s[slot].ttgt;
+                    unpack_cell(S.s[slot].tcell, tcr, tct, tcp);
+                    unpack_face(S.s[slot].tface, tft, tfi);
+                    // load the direction unconditionally (one round trip with the rest of the record)
+                    const double ldx = S.s[slot].dx, ldy = S.s[slot].dy, ldz = S.s[slot].dz;
+                    const bool peel = (mode == S_PEEL);
+                    nx = peel ? R.det0 : ldx; ny = peel ? R.det1 : ldy; nz = peel ? R.det2 : ldz;
                     seg_cross = 0;
                     have = true;
                 }
@@ -180,22 +264,22 @@ __global__ __launch_bounds__(BLOCK) void k_trace(DevGrid G, DevRun R, Pool S, Li
             } else if (tacc + tau_cell > ttgt) {          // interaction in this cell (ARTES.f90:705-720)
                 const double s = (ttgt - tacc) / k;
                 const double px = tx + s * nx, py = ty + s * ny, pz = tz + s * nz;
-                S.px[slot] = px; S.py[slot] = py; S.pz[slot] = pz;
-                S.pcell[slot] = pack_cell(tcr, tct, tcp);
-                S.pface[slot] = 0;
+                S.s[slot].px = px; S.s[slot].py = py; S.s[slot].pz = pz;
+                S.s[slot].pcell = pack_cell(tcr, tct, tcp);
+                S.s[slot].pface = 0;
                 // scattering-loop head (ARTES.f90:788-813)
-                Rng rng; rng.s0 = S.r0[slot]; rng.s1 = S.r1[slot];
+                Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
                 bool stop = !R.photon_scattering;
                 if (!stop) stop = rng.uni() < R.fstop;
                 if (!stop) {
                     const double alb = G.albedo[tcr + G.nr * (tct + G.ntheta * tcp)];
                     if (alb < 1.0 && alb > 0.0) {
                         const double gamma = alb / (1.0 - R.fstop);
-                        S.s0[slot] *= gamma; S.s1[slot] *= gamma; S.s2[slot] *= gamma; S.s3[slot] *= gamma;
+                        S.s[slot].s0 *= gamma; S.s[slot].s1 *= gamma; S.s[slot].s2 *= gamma; S.s[slot].s3 *= gamma;
                     }
-                    if (S.s0[slot] <= R.pmin) stop = true;
+                    if (S.s[slot].s0 <= R.pmin) stop = true;
                 }
-                S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+                S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
                 if (stop) {
                     end = S_END_ABS;
                 } else {                                   // peel-off trace (ARTES.f90:4722-4761)
@@ -212,9 +296,9 @@ __global__ __launch_bounds__(BLOCK) void k_trace(DevGrid G, DevRun R, Pool S, Li
                 if (o.exit) {
                     end = S_END_EXIT;
                 } else if (surf) {
-                    Rng rng; rng.s0 = S.r0[slot]; rng.s1 = S.r1[slot];
+                    Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
                     const double xi = rng.uni();
-                    S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+                    S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
                     if (xi > R.surface_albedo) end = S_END_ABS;
                     else { log_err(R, 62); end = S_END_DROP; }
                 } else {
@@ -227,14 +311,14 @@ __global__ __launch_bounds__(BLOCK) void k_trace(DevGrid G, DevRun R, Pool S, Li
             if (o.err) log_err(R, mode == S_FIRST ? 2 : 43);
             if (o.exit || o.err || surf) {
                 if (mode == S_PEEL) {
-                    S.tacc[slot] = tacc;
+                    S.s[slot].tacc = tacc;
                     end = S_PEEL_DONE | (o.exit ? FLAG_EXIT : 0) | (o.err ? FLAG_ERR : 0);
                 } else {   // forced first interaction (ARTES.f90:658-685)
                     const double tau_first = tacc;
                     if (tau_first < 1.e-6 && !surf) {
                         end = S_END_DROP;
                     } else {
-                        Rng rng; rng.s0 = S.r0[slot]; rng.s1 = S.r1[slot];
+                        Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
                         const double xi = rng.uni();
                         double tau;
                         if (tau_first < 1.e-6) {
@@ -242,14 +326,14 @@ __global__ __launch_bounds__(BLOCK) void k_trace(DevGrid G, DevRun R, Pool S, Li
                         } else if (tau_first < 50.0) {
                             const double e = 1.0 - exp(-tau_first);
                             tau = -log(1.0 - xi * e);
-                            S.s0[slot] *= e; S.s1[slot] *= e; S.s2[slot] *= e; S.s3[slot] *= e;
+                            S.s[slot].s0 *= e; S.s[slot].s1 *= e; S.s[slot].s2 *= e; S.s[slot].s3 *= e;
                         } else {
                             tau = -log(1.0 - xi);
                         }
-                        S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
-                        tx = S.px[slot]; ty = S.py[slot]; tz = S.pz[slot];
-                        unpack_cell(S.pcell[slot], tcr, tct, tcp);
-                        unpack_face(S.pface[slot], tft, tfi);
+                        S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
+                        tx = S.s[slot].px; ty = S.s[slot].py; tz = S.s[slot].pz;
+                        unpack_cell(S.s[slot].pcell, tcr, tct, tcp);
+                        unpack_face(S.s[slot].pface, tft, tfi);
                         tacc = 0.0; ttgt = tau;
                         mode = S_PROP;
                     }
@@ -259,8 +343,8 @@ __global__ __launch_bounds__(BLOCK) void k_trace(DevGrid G, DevRun R, Pool S, Li
             }
         }
         if (end) {
-            S.mode[slot] = end;
-            S.ncross[slot] += seg_cross;
+            S.s[slot].mode = end;
+            S.s[slot].ncross += seg_cross;
             have = false;
         }
         }   // have
@@ -278,29 +362,29 @@ __global__ __launch_bounds__(BLOCK) void k_trace(DevGrid G, DevRun R, Pool S, Li
 
 // park the packet in a new propagation trace starting at its position
 __device__ __forceinline__ void start_prop(const Pool& S, int slot, double tau) {
-    S.tx[slot] = S.px[slot]; S.ty[slot] = S.py[slot]; S.tz[slot] = S.pz[slot];
-    S.tcell[slot] = S.pcell[slot];
-    S.tface[slot] = S.pface[slot];
-    S.tacc[slot] = 0.0;
-    S.ttgt[slot] = tau;
-    S.mode[slot] = S_PROP;
+    S.s[slot].tx = S.s[slot].px; S.s[slot].ty = S.s[slot].py; S.s[slot].tz = S.s[slot].pz;
+    S.s[slot].tcell = S.s[slot].pcell;
+    S.s[slot].tface = S.s[slot].pface;
+    S.s[slot].tacc = 0.0;
+    S.s[slot].ttgt = tau;
+    S.s[slot].mode = S_PROP;
 }
 
 // one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended)
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
                                          size_t plane, uint32_t& c_scat, uint32_t& c_det) {
     {
-        const int m = S.mode[slot];
-        if (m & FLAG_ERR) { S.mode[slot] = S_END_DROP; return 2; }
-        const double px = S.px[slot], py = S.py[slot], pz = S.pz[slot];
-        double dx = S.dx[slot], dy = S.dy[slot], dz = S.dz[slot];
-        double st[4] = {S.s0[slot], S.s1[slot], S.s2[slot], S.s3[slot]};
+        const int m = S.s[slot].mode;
+        if (m & FLAG_ERR) { S.s[slot].mode = S_END_DROP; return 2; }
+        const double px = S.s[slot].px, py = S.s[slot].py, pz = S.s[slot].pz;
+        double dx = S.s[slot].dx, dy = S.s[slot].dy, dz = S.s[slot].dz;
+        double st[4] = {S.s[slot].s0, S.s[slot].s1, S.s[slot].s2, S.s[slot].s3};
         int cr, ct, cp;
-        unpack_cell(S.pcell[slot], cr, ct, cp);
+        unpack_cell(S.s[slot].pcell, cr, ct, cp);
         const int cell = cr + G.nr * (ct + G.ntheta * cp);
         const int mid = G.matid[cell];
         const double* __restrict__ P = G.mats + (size_t)mid * MAT_DOUBLES;
-        const double tau_peel = S.tacc[slot];
+        const double tau_peel = S.s[slot].tacc;
         bool drop = false;
         if ((m & FLAG_EXIT) && tau_peel < 50.0) {
             const double w = exp(-tau_peel);
@@ -349,14 +433,14 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                     } else {
                         const int pix = iy * R.nx + ix;
                         const double v[4] = {w * so[0], -w * so[1], w * so[2], w * so[3]};   // -Q: ARTES.f90:4956
-                        const int cur = S.cur_pix[slot];
-                        double cs[4] = {S.cs0[slot], S.cs1[slot], S.cs2[slot], S.cs3[slot]};
+                        const int cur = S.s[slot].cur_pix;
+                        double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
                         if (pix != cur) {
                             if (cur >= 0) {
 #pragma unroll
                                 for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
                             }
-                            S.cur_pix[slot] = pix;
+                            S.s[slot].cur_pix = pix;
                             cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
                         }
 #pragma unroll
@@ -366,9 +450,9 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                             cs[q] += v[q];
                         }
                         unsafeAtomicAdd(&det[8 * plane + pix], 1.0);
-                        S.cs0[slot] = cs[0]; S.cs1[slot] = cs[1]; S.cs2[slot] = cs[2]; S.cs3[slot] = cs[3];
-                        S.pt0[slot] += v[0]; S.pt1[slot] += v[1]; S.pt2[slot] += v[2]; S.pt3[slot] += v[3];
-                        S.peel_sum[slot] += wI;
+                        S.s[slot].cs0 = cs[0]; S.s[slot].cs1 = cs[1]; S.s[slot].cs2 = cs[2]; S.s[slot].cs3 = cs[3];
+                        S.s[slot].pt0 += v[0]; S.s[slot].pt1 += v[1]; S.s[slot].pt2 += v[2]; S.s[slot].pt3 += v[3];
+                        S.s[slot].peel_sum += wI;
                         c_det++;
                     }
                 } else {
@@ -376,11 +460,11 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                 }
             }
         }
-        if (drop) { S.mode[slot] = S_END_DROP; return 2; }
+        if (drop) { S.s[slot].mode = S_END_DROP; return 2; }
         // scatter_photon + polarization_rotation (ARTES.f90:819-846)
         c_scat++;
-        S.nscat[slot] += 1;
-        Rng rng; rng.s0 = S.r0[slot]; rng.s1 = S.r1[slot];
+        S.s[slot].nscat += 1;
+        Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
         double alpha, beta;
         sample_angles(G, R, G.cums + (size_t)mid * CUM_DOUBLES, rng, st, alpha, beta);
         double e0, e1, e2;
@@ -390,16 +474,16 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         if (fabs(alpha) < 1.0) {
             double sn[4];
             polarization_rotation(R, alpha, beta, st, sc, dz, e2, sn, false);
-            S.s0[slot] = sn[0]; S.s1[slot] = sn[1]; S.s2[slot] = sn[2]; S.s3[slot] = sn[3];
-            S.dx[slot] = e0; S.dy[slot] = e1; S.dz[slot] = e2;
+            S.s[slot].s0 = sn[0]; S.s[slot].s1 = sn[1]; S.s[slot].s2 = sn[2]; S.s[slot].s3 = sn[3];
+            S.s[slot].dx = e0; S.s[slot].dy = e1; S.s[slot].dz = e2;
             const double xi = rng.uni();
-            S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
+            S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
             start_prop(S, slot, -log(1.0 - xi));
             return 1;
         } else {
             log_err(R, 50);
-            S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
-            S.mode[slot] = S_END_DROP;
+            S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
+            S.s[slot].mode = S_END_DROP;
             return 2;
         }
     }
@@ -437,25 +521,25 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
     const int lane = threadIdx.x & 63;
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
         const int slot = i < n ? L.emit[i] : -1;
-        const int m = slot >= 0 ? S.mode[slot] : S_RETIRED;
+        const int m = slot >= 0 ? S.s[slot].mode : S_RETIRED;
         if (m == S_END_EXIT || m == S_END_ABS || m == S_END_DROP) {
             if (m == S_END_EXIT) c_exit++;
             else if (m == S_END_ABS) c_abs++;
             else c_drop++;
-            const int cur = S.cur_pix[slot];
+            const int cur = S.s[slot].cur_pix;
             if (cur >= 0) {
-                unsafeAtomicAdd(&det[12 * plane + cur], S.cs0[slot] * S.cs0[slot]);
-                unsafeAtomicAdd(&det[13 * plane + cur], S.cs1[slot] * S.cs1[slot]);
-                unsafeAtomicAdd(&det[14 * plane + cur], S.cs2[slot] * S.cs2[slot]);
-                unsafeAtomicAdd(&det[15 * plane + cur], S.cs3[slot] * S.cs3[slot]);
+                unsafeAtomicAdd(&det[12 * plane + cur], S.s[slot].cs0 * S.s[slot].cs0);
+                unsafeAtomicAdd(&det[13 * plane + cur], S.s[slot].cs1 * S.s[slot].cs1);
+                unsafeAtomicAdd(&det[14 * plane + cur], S.s[slot].cs2 * S.s[slot].cs2);
+                unsafeAtomicAdd(&det[15 * plane + cur], S.s[slot].cs3 * S.s[slot].cs3);
             }
-            const double a0 = S.pt0[slot], a1 = S.pt1[slot], a2 = S.pt2[slot], a3 = S.pt3[slot];
+            const double a0 = S.s[slot].pt0, a1 = S.s[slot].pt1, a2 = S.s[slot].pt2, a3 = S.s[slot].pt3;
             t2[0] += a0 * a0; t2[1] += a1 * a1; t2[2] += a2 * a2; t2[3] += a3 * a3;
             if constexpr (TRACE) {
-                double* rr = R.rec + (size_t)(S.pid[slot] - R.first) * 4;
-                rr[0] = S.peel_sum[slot];
-                rr[1] = (double)S.nscat[slot];
-                rr[2] = (double)S.ncross[slot];
+                double* rr = R.rec + (size_t)(S.s[slot].pid - R.first) * 4;
+                rr[0] = S.s[slot].peel_sum;
+                rr[1] = (double)S.s[slot].nscat;
+                rr[2] = (double)S.s[slot].ncross;
                 rr[3] = (double)(m - S_END_EXIT + 1);   // 1 exit, 2 absorbed, 3 dropped
             }
         }
@@ -471,7 +555,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
             k = base + __popcll(mask & ((1ULL << lane) - 1ULL));
         }
         const bool emit = need && k < R.n;
-        if (need && !emit) S.mode[slot] = S_RETIRED;
+        if (need && !emit) S.s[slot].mode = S_RETIRED;
         if (emit) {
         c_pkt++;
         const unsigned long long pid = R.first + k;
@@ -517,23 +601,23 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
                 if (ph > G.phif[j] && ph < hi) { cp = j; break; }
             }
         }
-        S.pid[slot] = pid;
-        S.r0[slot] = rng.s0; S.r1[slot] = rng.s1;
-        S.px[slot] = px; S.py[slot] = py; S.pz[slot] = pz;
-        S.dx[slot] = dx; S.dy[slot] = dy; S.dz[slot] = dz;
-        S.s0[slot] = 1.0; S.s1[slot] = 0.0; S.s2[slot] = 0.0; S.s3[slot] = 0.0;
+        S.s[slot].pid = pid;
+        S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
+        S.s[slot].px = px; S.s[slot].py = py; S.s[slot].pz = pz;
+        S.s[slot].dx = dx; S.s[slot].dy = dy; S.s[slot].dz = dz;
+        S.s[slot].s0 = 1.0; S.s[slot].s1 = 0.0; S.s[slot].s2 = 0.0; S.s[slot].s3 = 0.0;
         const int pc = pack_cell(cr, ct, cp), pf = pack_face(1, G.nr);
-        S.pcell[slot] = pc; S.pface[slot] = pf;
-        S.tx[slot] = px; S.ty[slot] = py; S.tz[slot] = pz;
-        S.tcell[slot] = pc; S.tface[slot] = pf;
-        S.tacc[slot] = 0.0; S.ttgt[slot] = 0.0;
-        S.cs0[slot] = S.cs1[slot] = S.cs2[slot] = S.cs3[slot] = 0.0;
-        S.pt0[slot] = S.pt1[slot] = S.pt2[slot] = S.pt3[slot] = 0.0;
-        S.peel_sum[slot] = 0.0;
-        S.cur_pix[slot] = -1;
-        S.nscat[slot] = 0;
-        S.ncross[slot] = 0;
-        S.mode[slot] = S_FIRST;
+        S.s[slot].pcell = pc; S.s[slot].pface = pf;
+        S.s[slot].tx = px; S.s[slot].ty = py; S.s[slot].tz = pz;
+        S.s[slot].tcell = pc; S.s[slot].tface = pf;
+        S.s[slot].tacc = 0.0; S.s[slot].ttgt = 0.0;
+        S.s[slot].cs0 = S.s[slot].cs1 = S.s[slot].cs2 = S.s[slot].cs3 = 0.0;
+        S.s[slot].pt0 = S.s[slot].pt1 = S.s[slot].pt2 = S.s[slot].pt3 = 0.0;
+        S.s[slot].peel_sum = 0.0;
+        S.s[slot].cur_pix = -1;
+        S.s[slot].nscat = 0;
+        S.s[slot].ncross = 0;
+        S.s[slot].mode = S_FIRST;
         }   // emit
         wave_append(emit, slot, L.trace_out, L.trace_out_n);
     }
@@ -556,7 +640,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
 __global__ void k_init(Pool S, int* emit, int* emit_n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < S.P) {
-        S.mode[i] = S_FRESH;
+        S.s[i].mode = S_FRESH;
         emit[i] = i;
     }
     if (i == 0) *emit_n = S.P;

@@ -210,23 +210,11 @@ static bool use_event_engine() {
 static int32_t ensure_pool(artes_grid* g) {
     if (g->pool_mem) return 0;
     const char* env = getenv("ARTES_POOL");
-    long long P = env ? atoll(env) : (long long)g->num_cus * 8192;
+    long long P = env ? atoll(env) : (long long)g->num_cus * 16384;
     P = std::max<long long>(1024, std::min<long long>(P, 1LL << 26));
-    const int nd = 24, nu = 3, ni = 8;   // doubles, u64, int32 arrays in Pool
-    const size_t bytes = (size_t)P * (nd * 8 + nu * 8 + ni * 4);
-    HIP_TRY(hipMalloc(&g->pool_mem, bytes));
-    char* base = (char*)g->pool_mem;
-    auto take_d = [&](double*& ptr) { ptr = (double*)base; base += (size_t)P * 8; };
-    auto take_u = [&](unsigned long long*& ptr) { ptr = (unsigned long long*)base; base += (size_t)P * 8; };
-    auto take_i = [&](int*& ptr) { ptr = (int*)base; base += (size_t)P * 4; };
-    Pool& S = g->pool;
-    S.P = (int)P;
-    double** dptrs[] = {&S.px, &S.py, &S.pz, &S.dx, &S.dy, &S.dz, &S.s0, &S.s1, &S.s2, &S.s3, &S.tx, &S.ty, &S.tz,
-                        &S.tacc, &S.ttgt, &S.cs0, &S.cs1, &S.cs2, &S.cs3, &S.pt0, &S.pt1, &S.pt2, &S.pt3, &S.peel_sum};
-    for (double** d : dptrs) take_d(*d);
-    take_u(S.r0); take_u(S.r1); take_u(S.pid);
-    int** iptrs[] = {&S.pcell, &S.pface, &S.tcell, &S.tface, &S.mode, &S.cur_pix, &S.nscat, &S.ncross};
-    for (int** d : iptrs) take_i(*d);
+    HIP_TRY(hipMalloc(&g->pool_mem, (size_t)P * sizeof(Slot)));
+    g->pool.P = (int)P;
+    g->pool.s = (Slot*)g->pool_mem;
     HIP_TRY(hipMalloc((void**)&g->d_lists[0], (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_lists[1], (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_event, (size_t)P * 4));
@@ -236,12 +224,28 @@ static int32_t ensure_pool(artes_grid* g) {
     HIP_TRY(hipMalloc((void**)&g->d_next, sizeof(unsigned long long)));
     HIP_TRY(hipHostMalloc((void**)&g->h_count, 64, hipHostMallocDefault));
     HIP_TRY(hipEventCreateWithFlags(&g->ev_poll, hipEventDisableTiming));
-    const bool g3d = (g->T.ntheta > 1 || g->T.nphi > 1);
-    int per_cu = 0;
-    if (g3d) HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<true>, BLOCK, 0));
-    else HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false>, BLOCK, 0));
-    g->trace_blocks = std::max(1, per_cu) * g->num_cus;
     return 0;
+}
+
+template <bool G3D, int WPE, bool LDS>
+static void launch_trace(artes_grid* g, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
+    const size_t lds = LDS ? face_table_bytes(G.nr, G.ntheta, G.nphi) : 0;
+    int per_cu = 0;
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, WPE, LDS>, BLOCK, lds);
+    g->trace_blocks = std::max(1, per_cu) * g->num_cus;
+    hipLaunchKernelGGL((k_trace<G3D, WPE, LDS>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+}
+
+template <bool G3D>
+static void launch_trace_any(artes_grid* g, int wpe, bool lds, const DevGrid& G, const DevRun& R, const Lists& L,
+                             hipStream_t stream) {
+    if (lds) {
+        if (wpe == 5) launch_trace<G3D, 5, true>(g, G, R, L, stream);
+        else launch_trace<G3D, 4, true>(g, G, R, L, stream);
+    } else {
+        if (wpe == 5) launch_trace<G3D, 5, false>(g, G, R, L, stream);
+        else launch_trace<G3D, 4, false>(g, G, R, L, stream);
+    }
 }
 
 template <bool G3D>
@@ -254,6 +258,11 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     HIP_TRY(hipMemsetAsync(g->d_next, 0, sizeof(unsigned long long), stream));
     int* cnt = g->d_counts;
     const int side_blocks = std::max(1, g->num_cus * 8);
+    const char* we = getenv("ARTES_WPE");
+    const int wpe = we ? atoi(we) : 5;
+    // face tables go to LDS unless they would cut the trace kernel's occupancy
+    const char* le = getenv("ARTES_LDS");
+    const bool use_lds = (le ? atoi(le) != 0 : true) && face_table_bytes(G.nr, G.ntheta, G.nphi) <= 32768;
     auto lists = [&](int in) {
         Lists L;
         L.trace_in = g->d_lists[in]; L.trace_in_n = cnt + in;
@@ -277,7 +286,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const long long max_it = 2000000LL;
     for (;;) {
         Lists L = lists(in);
-        hipLaunchKernelGGL((k_trace<G3D>), dim3(g->trace_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+        launch_trace_any<G3D>(g, wpe, use_lds, G, R, L, stream);
         hipLaunchKernelGGL(k_event, dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
         if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
         else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
@@ -339,6 +348,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.stellar_direction = p->stellar_direction;
     const char* env = getenv("ARTES_DEFER");
     R.defer = env ? atoi(env) : 16;
+    const char* rf = getenv("ARTES_REFILL");
+    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : 32;
+    const char* sq = getenv("ARTES_STATIC");   // statically split share of the trace list, in 1/64
+    R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : 32;
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)
     R.det1 = sin(p->det_theta) * sin(p->det_phi);
     R.det2 = cos(p->det_theta);
