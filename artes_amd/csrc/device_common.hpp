@@ -108,15 +108,16 @@ __device__ __forceinline__ double sin_b(double x) { double s, c; sincos_bounded(
 
 // ------------------------------------------------------------- geometry ---
 // quadratic_equation (ARTES.f90:4154-4173)
+// roots of a s^2 + b s + c = 0 in the cancellation-free form; 0 where a root does not
+// exist (negative discriminant, degenerate a or q).  Straight-line code: every lane of a
+// wave evaluates it the same way, the conditions only select.
 __device__ __forceinline__ void quad_roots(double a, double b, double c, double& s0, double& s1) {
-    s0 = 0.0;
-    s1 = 0.0;
     const double disc = b * b - 4.0 * a * c;
-    if (disc >= 0.0) {
-        const double q = -0.5 * (b + copysign(sqrt(disc), b));
-        if (fabs(a) > 1.e-100) s0 = q / a;
-        if (fabs(q) > 1.e-100) s1 = c / q;
-    }
+    const bool ok = disc >= 0.0;
+    const double q = -0.5 * (b + copysign(sqrt(ok ? disc : 0.0), b));
+    const double r0 = q / a, r1 = c / q;
+    s0 = (ok && fabs(a) > 1.e-100) ? r0 : 0.0;
+    s1 = (ok && fabs(q) > 1.e-100) ? r1 : 0.0;
 }
 // root selection block of cell_face (e.g. ARTES.f90:2897-2907)
 __device__ __forceinline__ double pick_root(double s0, double s1, double tol) {
@@ -139,14 +140,9 @@ __device__ __forceinline__ double cone_distance(const DevGrid& G, int f, double 
     double s0, s1;
     quad_roots(qa, qb, qc, s0, s1);
     const double th = G.thetaf[f];
-    if (s0 > 1.e-15) {
-        const double zt = z + s0 * n2;
-        if ((zt > 0.0 && th > HALF_PI) || (zt < 0.0 && th < HALF_PI)) s0 = 0.0;
-    }
-    if (s1 > 1.e-15) {
-        const double zt = z + s1 * n2;
-        if ((zt > 0.0 && th > HALF_PI) || (zt < 0.0 && th < HALF_PI)) s1 = 0.0;
-    }
+    const double z0 = z + s0 * n2, z1 = z + s1 * n2;
+    if (s0 > 1.e-15 && ((z0 > 0.0 && th > HALF_PI) || (z0 < 0.0 && th < HALF_PI))) s0 = 0.0;
+    if (s1 > 1.e-15 && ((z1 > 0.0 && th > HALF_PI) || (z1 < 0.0 && th < HALF_PI))) s1 = 0.0;
     return pick_root(s0, s1, tol);
 }
 
@@ -165,59 +161,51 @@ template <bool G3D>
 __device__ __forceinline__ void cell_face(const DevGrid& G, const DevRun& R, double x, double y, double z,
                                           double n0, double n1, double n2, int ft, int fi, int cr, int ct, int cp,
                                           Step& o) {
+    // Every candidate face is evaluated unconditionally and the reference's case split
+    // (same face / cone / 90-degree plane / no face) only selects among the results:
+    // lanes of a wave sit on different face kinds, and branching on them would run the
+    // divergent variants one after another.
     const double qa = G.ax2 * n0 * n0 + G.by2 * n1 * n1 + G.cz2 * n2 * n2;
     const double qb = 2.0 * (G.ax2 * x * n0 + G.by2 * y * n1 + G.cz2 * z * n2);
     const double S = G.ax2 * x * x + G.by2 * y * y + G.cz2 * z * z;
     double s0, s1;
-    double d_rin = 0.0, d_rout = 0.0;
-    if (!(ft == 1 && fi == cr)) {                      // inner sphere r_cell
-        quad_roots(qa, qb, S - G.rf2[cr], s0, s1);
-        d_rin = pick_root(s0, s1, 1.e-15);
-    }
-    {                                                  // outer sphere r_cell+1 (same face: 1e-3)
-        quad_roots(qa, qb, S - G.rf2[cr + 1], s0, s1);
-        d_rout = pick_root(s0, s1, (ft == 1 && fi == cr + 1) ? 1.e-3 : 1.e-15);
-    }
+    quad_roots(qa, qb, S - G.rf2[cr], s0, s1);        // inner sphere r_cell
+    const double d_rin = (ft == 1 && fi == cr) ? 0.0 : pick_root(s0, s1, 1.e-15);
+    quad_roots(qa, qb, S - G.rf2[cr + 1], s0, s1);    // outer sphere r_cell+1 (same face: 1e-3)
+    const double d_rout = pick_root(s0, s1, (ft == 1 && fi == cr + 1) ? 1.e-3 : 1.e-15);
     double d_tin = 0.0, d_tout = 0.0, d_pin = 0.0, d_pout = 0.0;
     int pout = 0;
     if constexpr (G3D) {
         const bool on_t = (ft == 2);
-        if (ct != 0) {                                 // inner theta face (index ct)
-            if (on_t && fi == ct) {
-                if (G.thetaf[ct] > HALF_PI && G.tplane[ct] == 1) d_tin = cone_distance(G, ct, x, y, z, n0, n1, n2, 1.e-3);
-            } else if (G.tplane[ct] == 1) {
-                d_tin = cone_distance(G, ct, x, y, z, n0, n1, n2, 1.e-15);
-            } else {
-                if (-z / n2 > 0.0 && n2 > 1.e-15) d_tin = -z / n2;
-            }
+        const double zp = -z / n2;                     // the 90-degree face is the plane z = 0
+        {                                              // inner theta face (index ct)
+            const bool same = on_t && fi == ct;
+            const double dc = cone_distance(G, ct, x, y, z, n0, n1, n2, same ? 1.e-3 : 1.e-15);
+            double d;
+            if (G.tplane[ct] == 1) d = (!same || G.thetaf[ct] > HALF_PI) ? dc : 0.0;
+            else d = (!same && zp > 0.0 && n2 > 1.e-15) ? zp : 0.0;
+            d_tin = (ct != 0) ? d : 0.0;
         }
-        if (ct + 1 != G.ntheta) {                      // outer theta face (index ct+1)
-            if (on_t && fi == ct + 1) {
-                if (G.thetaf[ct + 1] < HALF_PI && G.tplane[ct + 1] == 1) d_tout = cone_distance(G, ct + 1, x, y, z, n0, n1, n2, 1.e-3);
-            } else if (G.tplane[ct + 1] == 1) {
-                d_tout = cone_distance(G, ct + 1, x, y, z, n0, n1, n2, 1.e-15);
-            } else {
-                if (-z / n2 > 0.0 && n2 < -1.e-15) d_tout = -z / n2;
-            }
+        {                                              // outer theta face (index ct+1)
+            const bool same = on_t && fi == ct + 1;
+            const double dc = cone_distance(G, ct + 1, x, y, z, n0, n1, n2, same ? 1.e-3 : 1.e-15);
+            double d;
+            if (G.tplane[ct + 1] == 1) d = (!same || G.thetaf[ct + 1] < HALF_PI) ? dc : 0.0;
+            else d = (!same && zp > 0.0 && n2 < -1.e-15) ? zp : 0.0;
+            d_tout = (ct + 1 != G.ntheta) ? d : 0.0;
         }
         if (G.nphi > 1) {                              // phi half-planes (ARTES.f90:3292-3350)
             pout = (cp + 1 == G.nphi) ? 0 : cp + 1;
             const bool on_p = (ft == 3);
-            double sp0 = 0.0;
-            if (!(on_p && fi == cp)) {
-                const double den = G.b * n1 * G.phic[cp] - G.a * n0 * G.phis[cp];
-                if (fabs(den) > 0.0) {
-                    sp0 = (G.a * x * G.phis[cp] - G.b * y * G.phic[cp]) / den;
-                    if (sp0 > 1.e-15 && sp0 < 1.e100) d_pin = sp0;
-                }
-            }
-            if (!(on_p && fi == pout)) {
-                const double den = G.b * n1 * G.phic[pout] - G.a * n0 * G.phis[pout];
-                if (fabs(den) > 0.0) {
-                    const double sp1 = (G.a * x * G.phis[pout] - G.b * y * G.phic[pout]) / den;
-                    if (sp1 > 1.e-15 && sp0 < 1.e100) d_pout = sp1;   // sic: sp0 (ARTES.f90:3318, 3346)
-                }
-            }
+            const double den0 = G.b * n1 * G.phic[cp] - G.a * n0 * G.phis[cp];
+            const double num0 = G.a * x * G.phis[cp] - G.b * y * G.phic[cp];
+            const double den1 = G.b * n1 * G.phic[pout] - G.a * n0 * G.phis[pout];
+            const double num1 = G.a * x * G.phis[pout] - G.b * y * G.phic[pout];
+            const double q0 = num0 / den0, q1 = num1 / den1;
+            const double sp0 = (!(on_p && fi == cp) && fabs(den0) > 0.0) ? q0 : 0.0;
+            d_pin = (sp0 > 1.e-15 && sp0 < 1.e100) ? sp0 : 0.0;
+            const bool ok1 = !(on_p && fi == pout) && fabs(den1) > 0.0;
+            d_pout = (ok1 && q1 > 1.e-15 && sp0 < 1.e100) ? q1 : 0.0;   // sic: sp0 (ARTES.f90:3318, 3346)
         }
     }
     // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
