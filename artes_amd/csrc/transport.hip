@@ -24,6 +24,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "device_common.hpp"
 #include "kernel_persistent.hpp"
@@ -91,7 +92,30 @@ struct artes_grid {
     hipEvent_t ev_poll = nullptr;
     int trace_blocks = 0;
     long long last_iterations = 0;
+    // per-launch timing (artes_set_profiling)
+    bool prof = false;
+    std::vector<hipEvent_t> prof_ev;     // start/end pairs
+    std::vector<int> prof_kind;
+    size_t prof_used = 0;
 };
+
+// run `launch` between two recorded events when profiling is on
+template <class F>
+static void timed(artes_grid* g, int kind, hipStream_t s, F&& launch) {
+    if (!g->prof) { launch(); return; }
+    const size_t i = g->prof_used;
+    while (g->prof_ev.size() < 2 * (i + 1)) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) { launch(); return; }
+        g->prof_ev.push_back(e);
+    }
+    if (g->prof_kind.size() < i + 1) g->prof_kind.resize(i + 1);
+    hipEventRecord(g->prof_ev[2 * i], s);
+    launch();
+    hipEventRecord(g->prof_ev[2 * i + 1], s);
+    g->prof_kind[i] = kind;
+    g->prof_used = i + 1;
+}
 
 static thread_local std::string g_last_error;
 
@@ -143,6 +167,7 @@ void artes_grid_destroy(artes_grid* g) {
         if (p) hipFree(p);
     if (g->h_count) hipHostFree(g->h_count);
     if (g->ev_poll) hipEventDestroy(g->ev_poll);
+    for (hipEvent_t e : g->prof_ev) hipEventDestroy(e);
     if (g->ev0) hipEventDestroy(g->ev0);
     if (g->ev1) hipEventDestroy(g->ev1);
     delete g;
@@ -233,7 +258,9 @@ static void launch_trace(artes_grid* g, const DevGrid& G, const DevRun& R, const
     int per_cu = 0;
     hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, WPE, LDS>, BLOCK, lds);
     g->trace_blocks = std::max(1, per_cu) * g->num_cus;
-    hipLaunchKernelGGL((k_trace<G3D, WPE, LDS>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+    timed(g, ARTES_K_TRACE, stream, [&] {
+        hipLaunchKernelGGL((k_trace<G3D, WPE, LDS>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+    });
 }
 
 template <bool G3D>
@@ -272,13 +299,20 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         L.grab = g->d_grab; L.next_pkt = g->d_next;
         return L;
     };
-    hipLaunchKernelGGL(k_init, dim3((P + 255) / 256), dim3(256), 0, stream, g->pool, g->d_emit, cnt + 3);
+    auto launch_emit = [&](const Lists& L) {
+        if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+        else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+    };
+    timed(g, ARTES_K_AUX, stream, [&] {
+        hipLaunchKernelGGL(k_init, dim3((P + 255) / 256), dim3(256), 0, stream, g->pool, g->d_emit, cnt + 3);
+    });
     // pre-iteration: fill the pool; emitted packets go to trace list 0
     {
         Lists L = lists(1);   // trace_out = list 0
-        if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
-        else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
-        hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + 1, cnt + 0, cnt + 2, cnt + 3, g->d_grab);
+        timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
+        timed(g, ARTES_K_AUX, stream, [&] {
+            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + 1, cnt + 0, cnt + 2, cnt + 3, g->d_grab);
+        });
     }
     HIP_TRY(hipGetLastError());
     int in = 0;
@@ -287,10 +321,13 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     for (;;) {
         Lists L = lists(in);
         launch_trace_any<G3D>(g, wpe, use_lds, G, R, L, stream);
-        hipLaunchKernelGGL(k_event, dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
-        if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
-        else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
-        hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + in, cnt + (1 - in), cnt + 2, cnt + 3, g->d_grab);
+        timed(g, ARTES_K_EVENT, stream, [&] {
+            hipLaunchKernelGGL(k_event, dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+        });
+        timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
+        timed(g, ARTES_K_AUX, stream, [&] {
+            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + in, cnt + (1 - in), cnt + 2, cnt + 3, g->d_grab);
+        });
         in = 1 - in;
         it++;
         if ((it & 7) == 0 || it < 4) {   // poll the live-packet count (trace list of the next iteration)
@@ -372,19 +409,23 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     } else if (n > 0) {
         uint64_t want = (n + BLOCK - 1) / BLOCK;
         int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)g->max_blocks));
-        if (rec) {
-            if (g3d) hipLaunchKernelGGL((transport_kernel<true, true>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
-            else hipLaunchKernelGGL((transport_kernel<false, true>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
-        } else {
-            if (g3d) hipLaunchKernelGGL((transport_kernel<true, false>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
-            else hipLaunchKernelGGL((transport_kernel<false, false>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
-        }
+        timed(g, ARTES_K_PERSISTENT, stream, [&] {
+            if (rec) {
+                if (g3d) hipLaunchKernelGGL((transport_kernel<true, true>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
+                else hipLaunchKernelGGL((transport_kernel<false, true>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
+            } else {
+                if (g3d) hipLaunchKernelGGL((transport_kernel<true, false>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
+                else hipLaunchKernelGGL((transport_kernel<false, false>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
+            }
+        });
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(g->ev1, stream));
     g->timed = true;
     const int rb = (int)((stride + 255) / 256);
-    hipLaunchKernelGGL(reduce_detector, dim3(rb), dim3(256), 0, stream, (const double*)g->d_copies, stride, plane, det_out);
+    timed(g, ARTES_K_AUX, stream, [&] {
+        hipLaunchKernelGGL(reduce_detector, dim3(rb), dim3(256), 0, stream, (const double*)g->d_copies, stride, plane, det_out);
+    });
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -469,6 +510,29 @@ int32_t artes_run_trace(artes_grid* g, const artes_run_params* p, uint64_t first
     if (n > (1ull << 24)) return fail(-22, "trace runs are limited to 2^24 packets");
     std::vector<double> det((size_t)16 * p->nx * p->ny, 0.0);
     return run_host(g, p, first, n, seed, det.data(), nullptr, nullptr, nullptr, records);
+}
+
+int32_t artes_set_profiling(artes_grid* g, int32_t on) {
+    if (!g) return fail(-22, "null grid");
+    g->prof = on != 0;
+    g->prof_used = 0;
+    return 0;
+}
+
+int32_t artes_kernel_times(artes_grid* g, double* ms, uint64_t* launches) {
+    if (!g || !ms) return fail(-22, "null argument");
+    for (int k = 0; k < ARTES_NUM_KERNELS; k++) { ms[k] = 0.0; if (launches) launches[k] = 0; }
+    if (g->prof_used == 0) return 0;
+    HIP_TRY(hipSetDevice(g->device));
+    HIP_TRY(hipEventSynchronize(g->prof_ev[2 * g->prof_used - 1]));
+    for (size_t i = 0; i < g->prof_used; i++) {
+        float t = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&t, g->prof_ev[2 * i], g->prof_ev[2 * i + 1]));
+        ms[g->prof_kind[i]] += (double)t;
+        if (launches) launches[g->prof_kind[i]] += 1;
+    }
+    g->prof_used = 0;
+    return 0;
 }
 
 double artes_last_kernel_ms(artes_grid* g) {

@@ -20,6 +20,9 @@ LIB_PATH = os.path.join(HERE, "lib", "libartes_hip.so")
 _lib = None
 
 
+KERNEL_NAMES = ("trace", "event", "emit", "aux", "persistent")   # ARTES_K_* order
+
+
 class EngineUnavailable(RuntimeError):
     pass
 
@@ -63,6 +66,10 @@ def lib():
     L.artes_run_trace.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64, dp]
     L.artes_last_kernel_ms.restype = C.c_double
     L.artes_last_kernel_ms.argtypes = [C.c_void_p]
+    L.artes_set_profiling.restype = C.c_int32
+    L.artes_set_profiling.argtypes = [C.c_void_p, C.c_int32]
+    L.artes_kernel_times.restype = C.c_int32
+    L.artes_kernel_times.argtypes = [C.c_void_p, dp, up]
     if L.artes_abi_version() != 1:
         raise EngineUnavailable("ABI version mismatch")
     _lib = L
@@ -146,6 +153,17 @@ class Grid:
 
     def last_kernel_ms(self) -> float:
         return lib().artes_last_kernel_ms(self.h)
+
+    def set_profiling(self, on: bool = True) -> None:
+        _check(lib().artes_set_profiling(self.h, int(bool(on))), "artes_set_profiling")
+
+    def kernel_times(self) -> dict:
+        """{kernel class: (summed ms, launches)} since the last call (profiling on)."""
+        ms = np.zeros(len(KERNEL_NAMES))
+        n = np.zeros(len(KERNEL_NAMES), dtype=np.uint64)
+        _check(lib().artes_kernel_times(self.h, ms.ctypes.data_as(C.POINTER(C.c_double)),
+                                        n.ctypes.data_as(C.POINTER(C.c_uint64))), "artes_kernel_times")
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(KERNEL_NAMES)}
 
     def close(self) -> None:
         if getattr(self, "h", None) and self.h.value:

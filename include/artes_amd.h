@@ -123,20 +123,36 @@ int32_t artes_run(artes_grid* grid, const artes_run_params* params,
                   uint64_t first_packet, uint64_t n_packets, uint64_t seed,
                   double* detector, double* totals, uint64_t* counters, uint64_t* err);
 
-/* Asynchronous device variant: outputs are DEVICE pointers (e.g. torch tensors)
- * that are accumulated into on `stream` (a hipStream_t, NULL = default stream);
- * nothing is synchronised, so the caller can all-reduce `detector_dev` with RCCL
- * on the same stream.  `kernel_ms` (may be NULL) receives nothing here; use
- * artes_last_kernel_ms after synchronising. */
+/* Device variant: outputs are DEVICE pointers (e.g. torch tensors) accumulated
+ * into on `stream` (a hipStream_t, NULL = default stream), so the caller can
+ * all-reduce `detector_dev` with RCCL on the same stream.  totals_dev holds only
+ * the four sum_p T_p^2 values (the sums T_p are the detector plane-0 totals).
+ * The event engine polls its live-packet count from the host every few
+ * iterations, so the call returns once the transport has drained; the final
+ * detector reduction is still in flight on `stream`. */
 int32_t artes_run_device(artes_grid* grid, const artes_run_params* params,
                          uint64_t first_packet, uint64_t n_packets, uint64_t seed,
                          double* detector_dev, double* totals_dev, uint64_t* counters_dev,
                          uint64_t* err_dev, void* stream);
 
-/* Duration in ms of the transport kernel of the most recent run on this grid,
- * measured with HIP events on the launch stream (valid once that stream has
- * been synchronised). */
+/* Duration in ms of the transport (all launches from emission to drain, without
+ * the final detector reduction) of the most recent run on this grid, measured
+ * with HIP events on the launch stream (valid once that stream has been
+ * synchronised). */
 double artes_last_kernel_ms(artes_grid* grid);
+
+/* Per-kernel launch timing (HIP events around every launch on the run's stream).
+ * artes_set_profiling(grid, 1) starts recording; artes_kernel_times waits for the
+ * recorded launches, writes the summed milliseconds and launch counts per kernel class
+ * (ARTES_K_*) and resets the accumulators.  Off by default (no events are recorded). */
+#define ARTES_K_TRACE       0   /* k_trace: cell-boundary tracing (the hot loop)      */
+#define ARTES_K_EVENT       1   /* k_event: peel-off contribution + scattering       */
+#define ARTES_K_EMIT        2   /* k_emit: packet close-out + emission               */
+#define ARTES_K_AUX         3   /* list rotation, pool init, detector-copy reduction */
+#define ARTES_K_PERSISTENT  4   /* the fused single-kernel engine (ARTES_ENGINE=persistent) */
+#define ARTES_NUM_KERNELS   5
+int32_t artes_set_profiling(artes_grid* grid, int32_t on);
+int32_t artes_kernel_times(artes_grid* grid, double* ms, uint64_t* launches);
 
 /* Debug: per-packet records for packets [first, first+n) (n <= 2^24):
  * rec[n][4] = { sum of peeled I weight, scatters, crossings, end state }.
