@@ -131,12 +131,16 @@ __device__ __forceinline__ double pick_root(double s0, double s1, double tol) {
 }
 
 // theta cone x^2+y^2 = z^2 tan^2(theta_f) with the nappe filter (ARTES.f90:3026-3064)
+template <bool OBL>
 __device__ __forceinline__ double cone_distance(const DevGrid& G, int f, double x, double y, double z,
                                                 double n0, double n1, double n2, double tol) {
+    // spheroid axis factors; exactly 1 for a spherical planet (OBL = false), where the
+    // products they appear in are exact and fold away
+    const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
     const double t2 = G.tan2[f];
-    const double qa = G.ax2 * n0 * n0 + G.by2 * n1 * n1 - G.cz2 * n2 * n2 * t2;
-    const double qb = 2.0 * (G.ax2 * x * n0 + G.by2 * y * n1 - G.cz2 * z * n2 * t2);
-    const double qc = G.ax2 * x * x + G.by2 * y * y - G.cz2 * z * z * t2;
+    const double qa = ax2 * n0 * n0 + by2 * n1 * n1 - cz2 * n2 * n2 * t2;
+    const double qb = 2.0 * (ax2 * x * n0 + by2 * y * n1 - cz2 * z * n2 * t2);
+    const double qc = ax2 * x * x + by2 * y * y - cz2 * z * z * t2;
     double s0, s1;
     quad_roots(qa, qb, qc, s0, s1);
     const double th = G.thetaf[f];
@@ -157,17 +161,19 @@ struct Step {
 // packet sits on use the reference's 1e-3 tolerance in the matching slot.  The
 // candidate set, tolerances and two-pass (>1e-9, then >1e-12) selection are the
 // reference's; DESIGN.md §3 walks through the equivalence.
-template <bool G3D>
+template <bool G3D, bool OBL = true>
 __device__ __forceinline__ void cell_face(const DevGrid& G, const DevRun& R, double x, double y, double z,
                                           double n0, double n1, double n2, int ft, int fi, int cr, int ct, int cp,
                                           Step& o) {
+    const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
+    const double ga = OBL ? G.a : 1.0, gb = OBL ? G.b : 1.0;
     // Every candidate face is evaluated unconditionally and the reference's case split
     // (same face / cone / 90-degree plane / no face) only selects among the results:
     // lanes of a wave sit on different face kinds, and branching on them would run the
     // divergent variants one after another.
-    const double qa = G.ax2 * n0 * n0 + G.by2 * n1 * n1 + G.cz2 * n2 * n2;
-    const double qb = 2.0 * (G.ax2 * x * n0 + G.by2 * y * n1 + G.cz2 * z * n2);
-    const double S = G.ax2 * x * x + G.by2 * y * y + G.cz2 * z * z;
+    const double qa = ax2 * n0 * n0 + by2 * n1 * n1 + cz2 * n2 * n2;
+    const double qb = 2.0 * (ax2 * x * n0 + by2 * y * n1 + cz2 * z * n2);
+    const double S = ax2 * x * x + by2 * y * y + cz2 * z * z;
     double s0, s1;
     quad_roots(qa, qb, S - G.rf2[cr], s0, s1);        // inner sphere r_cell
     const double d_rin = (ft == 1 && fi == cr) ? 0.0 : pick_root(s0, s1, 1.e-15);
@@ -180,7 +186,7 @@ __device__ __forceinline__ void cell_face(const DevGrid& G, const DevRun& R, dou
         const double zp = -z / n2;                     // the 90-degree face is the plane z = 0
         {                                              // inner theta face (index ct)
             const bool same = on_t && fi == ct;
-            const double dc = cone_distance(G, ct, x, y, z, n0, n1, n2, same ? 1.e-3 : 1.e-15);
+            const double dc = cone_distance<OBL>(G, ct, x, y, z, n0, n1, n2, same ? 1.e-3 : 1.e-15);
             double d;
             if (G.tplane[ct] == 1) d = (!same || G.thetaf[ct] > HALF_PI) ? dc : 0.0;
             else d = (!same && zp > 0.0 && n2 > 1.e-15) ? zp : 0.0;
@@ -188,7 +194,7 @@ __device__ __forceinline__ void cell_face(const DevGrid& G, const DevRun& R, dou
         }
         {                                              // outer theta face (index ct+1)
             const bool same = on_t && fi == ct + 1;
-            const double dc = cone_distance(G, ct + 1, x, y, z, n0, n1, n2, same ? 1.e-3 : 1.e-15);
+            const double dc = cone_distance<OBL>(G, ct + 1, x, y, z, n0, n1, n2, same ? 1.e-3 : 1.e-15);
             double d;
             if (G.tplane[ct + 1] == 1) d = (!same || G.thetaf[ct + 1] < HALF_PI) ? dc : 0.0;
             else d = (!same && zp > 0.0 && n2 < -1.e-15) ? zp : 0.0;
@@ -197,10 +203,10 @@ __device__ __forceinline__ void cell_face(const DevGrid& G, const DevRun& R, dou
         if (G.nphi > 1) {                              // phi half-planes (ARTES.f90:3292-3350)
             pout = (cp + 1 == G.nphi) ? 0 : cp + 1;
             const bool on_p = (ft == 3);
-            const double den0 = G.b * n1 * G.phic[cp] - G.a * n0 * G.phis[cp];
-            const double num0 = G.a * x * G.phis[cp] - G.b * y * G.phic[cp];
-            const double den1 = G.b * n1 * G.phic[pout] - G.a * n0 * G.phis[pout];
-            const double num1 = G.a * x * G.phis[pout] - G.b * y * G.phic[pout];
+            const double den0 = gb * n1 * G.phic[cp] - ga * n0 * G.phis[cp];
+            const double num0 = ga * x * G.phis[cp] - gb * y * G.phic[cp];
+            const double den1 = gb * n1 * G.phic[pout] - ga * n0 * G.phis[pout];
+            const double num1 = ga * x * G.phis[pout] - gb * y * G.phic[pout];
             const double q0 = num0 / den0, q1 = num1 / den1;
             const double sp0 = (!(on_p && fi == cp) && fabs(den0) > 0.0) ? q0 : 0.0;
             d_pin = (sp0 > 1.e-15 && sp0 < 1.e100) ? sp0 : 0.0;

@@ -209,7 +209,7 @@ __device__ __forceinline__ DevGrid stage_face_tables(const DevGrid& G, double* l
     return GL;
 }
 
-template <bool G3D, int WPE, bool LDS>
+template <bool G3D, bool OBL, int WPE, bool LDS>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G0, DevRun R, Pool S, Lists L) {
     extern __shared__ double s_tab[];
     const DevGrid G = LDS ? stage_face_tables(G0, s_tab) : G0;
@@ -220,6 +220,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
     TraceCursor cur = make_cursor(n, R.static_q64);
     bool have = false;
+#ifdef ARTES_DEBUG_LANES
+    unsigned long long dbg_steps = 0, dbg_lanes = 0, dbg_refills = 0;
+#endif
     int slot = -1, mode = 0, tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0;
     double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, ttgt = 0;
     uint32_t c_cross = 0, c_peel = 0, seg_cross = 0;
@@ -230,6 +233,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             const unsigned long long idle = __ballot(!have);
             if (__popcll(idle) >= R.refill || idle == __ballot(true)) {
                 const int my = wave_take(cur, L.grab, home, !have);
+#ifdef ARTES_DEBUG_LANES
+                dbg_refills++;
+#endif
                 if (!have && my >= 0) {
                     slot = L.trace_in[my];
                     mode = S.s[slot].mode;
@@ -247,17 +253,37 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             }
         }
         if (!__any(have)) break;
+#ifdef ARTES_DEBUG_LANES
+        dbg_steps++;
+        dbg_lanes += __popcll(__ballot(have));
+#endif
         int end = 0;   // 0: continue, else the slot's new mode
         if (have) {
         // ------------------------------------------------------------ trace step
         Step o;
-        cell_face<G3D>(G, R, tx, ty, tz, nx, ny, nz, tft, tfi, tcr, tct, tcp, o);
+        cell_face<G3D, OBL>(G, R, tx, ty, tz, nx, ny, nz, tft, tfi, tcr, tct, tcp, o);
         c_cross++;
         seg_cross++;
         const double k = G.kappa[tcr + G.nr * (tct + G.ntheta * tcp)];
+#ifdef ARTES_DEBUG_LANES
+        // timing probe: extra dependent FP64 work per step (R.defer iterations; result unused but kept)
+        double spin = o.d;
+        for (int q = 0; q < R.defer; q += 16) {
+#pragma unroll
+            for (int u = 0; u < 16; u++) spin = fma(spin, 1.0000001, 1e-30);
+        }
+        if (spin == 12345.678) log_err(R, 58);
+#endif
         const double tau_cell = o.d * k;
         const bool surf = (o.nft == 1 && o.nfi == G.cell_depth);
-        if (mode == S_PROP) {
+        const bool prop = (mode == S_PROP);
+        // common case for every trace kind: no interaction in this cell, no boundary event
+        const bool stop = o.err || o.exit || surf || (prop && tacc + tau_cell > ttgt);
+        if (!stop) {
+            tacc += tau_cell;
+            tx += o.d * nx; ty += o.d * ny; tz += o.d * nz;
+            tft = o.nft; tfi = o.nfi; tcr = o.ncr; tct = o.nct; tcp = o.ncp;
+        } else if (prop) {
             if (o.err) {
                 log_err(R, 3);
                 end = S_END_DROP;
@@ -269,18 +295,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 S.s[slot].pface = 0;
                 // scattering-loop head (ARTES.f90:788-813)
                 Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
-                bool stop = !R.photon_scattering;
-                if (!stop) stop = rng.uni() < R.fstop;
-                if (!stop) {
+                bool kill = !R.photon_scattering;
+                if (!kill) kill = rng.uni() < R.fstop;
+                if (!kill) {
                     const double alb = G.albedo[tcr + G.nr * (tct + G.ntheta * tcp)];
                     if (alb < 1.0 && alb > 0.0) {
                         const double gamma = alb / (1.0 - R.fstop);
                         S.s[slot].s0 *= gamma; S.s[slot].s1 *= gamma; S.s[slot].s2 *= gamma; S.s[slot].s3 *= gamma;
                     }
-                    if (S.s[slot].s0 <= R.pmin) stop = true;
+                    if (S.s[slot].s0 <= R.pmin) kill = true;
                 }
                 S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
-                if (stop) {
+                if (kill) {
                     end = S_END_ABS;
                 } else {                                   // peel-off trace (ARTES.f90:4722-4761)
                     c_peel++;
@@ -290,56 +316,45 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     tacc = 0.0;
                     mode = S_PEEL;
                 }
-            } else {
-                tx += o.d * nx; ty += o.d * ny; tz += o.d * nz;
-                tft = o.nft; tfi = o.nfi; tcr = o.ncr; tct = o.nct; tcp = o.ncp;
-                if (o.exit) {
-                    end = S_END_EXIT;
-                } else if (surf) {
+            } else if (o.exit) {                           // left the atmosphere
+                end = S_END_EXIT;
+            } else {                                       // reached the surface (ARTES.f90:755-774)
+                Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
+                const double xi = rng.uni();
+                S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
+                if (xi > R.surface_albedo) end = S_END_ABS;
+                else { log_err(R, 62); end = S_END_DROP; }
+            }
+        } else {   // S_FIRST or S_PEEL reached the boundary: total optical depth known
+            tacc += tau_cell;
+            if (o.err) log_err(R, mode == S_FIRST ? 2 : 43);
+            if (mode == S_PEEL) {
+                S.s[slot].tacc = tacc;
+                end = S_PEEL_DONE | (o.exit ? FLAG_EXIT : 0) | (o.err ? FLAG_ERR : 0);
+            } else {   // forced first interaction (ARTES.f90:658-685)
+                const double tau_first = tacc;
+                if (tau_first < 1.e-6 && !surf) {
+                    end = S_END_DROP;
+                } else {
                     Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
                     const double xi = rng.uni();
-                    S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
-                    if (xi > R.surface_albedo) end = S_END_ABS;
-                    else { log_err(R, 62); end = S_END_DROP; }
-                } else {
-                    tacc += tau_cell;
-                }
-            }
-        } else {   // S_FIRST or S_PEEL: accumulate optical depth to the boundary
-            tacc += tau_cell;
-            tx += o.d * nx; ty += o.d * ny; tz += o.d * nz;
-            if (o.err) log_err(R, mode == S_FIRST ? 2 : 43);
-            if (o.exit || o.err || surf) {
-                if (mode == S_PEEL) {
-                    S.s[slot].tacc = tacc;
-                    end = S_PEEL_DONE | (o.exit ? FLAG_EXIT : 0) | (o.err ? FLAG_ERR : 0);
-                } else {   // forced first interaction (ARTES.f90:658-685)
-                    const double tau_first = tacc;
-                    if (tau_first < 1.e-6 && !surf) {
-                        end = S_END_DROP;
+                    double tau;
+                    if (tau_first < 1.e-6) {
+                        tau = -log(1.0 - xi);
+                    } else if (tau_first < 50.0) {
+                        const double e = 1.0 - exp(-tau_first);
+                        tau = -log(1.0 - xi * e);
+                        S.s[slot].s0 *= e; S.s[slot].s1 *= e; S.s[slot].s2 *= e; S.s[slot].s3 *= e;
                     } else {
-                        Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
-                        const double xi = rng.uni();
-                        double tau;
-                        if (tau_first < 1.e-6) {
-                            tau = -log(1.0 - xi);
-                        } else if (tau_first < 50.0) {
-                            const double e = 1.0 - exp(-tau_first);
-                            tau = -log(1.0 - xi * e);
-                            S.s[slot].s0 *= e; S.s[slot].s1 *= e; S.s[slot].s2 *= e; S.s[slot].s3 *= e;
-                        } else {
-                            tau = -log(1.0 - xi);
-                        }
-                        S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
-                        tx = S.s[slot].px; ty = S.s[slot].py; tz = S.s[slot].pz;
-                        unpack_cell(S.s[slot].pcell, tcr, tct, tcp);
-                        unpack_face(S.s[slot].pface, tft, tfi);
-                        tacc = 0.0; ttgt = tau;
-                        mode = S_PROP;
+                        tau = -log(1.0 - xi);
                     }
+                    S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
+                    tx = S.s[slot].px; ty = S.s[slot].py; tz = S.s[slot].pz;
+                    unpack_cell(S.s[slot].pcell, tcr, tct, tcp);
+                    unpack_face(S.s[slot].pface, tft, tfi);
+                    tacc = 0.0; ttgt = tau;
+                    mode = S_PROP;
                 }
-            } else {
-                tft = o.nft; tfi = o.nfi; tcr = o.ncr; tct = o.nct; tcp = o.ncp;
             }
         }
         if (end) {
@@ -353,6 +368,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     }
     q_event.flush(L.event, L.event_n);
     q_emit.flush(L.emit, L.emit_n);
+#ifdef ARTES_DEBUG_LANES
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&R.err[60], dbg_steps);
+        atomicAdd(&R.err[61], dbg_lanes);
+        atomicAdd(&R.err[59], dbg_refills);
+    }
+#endif
     const unsigned long long w = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);
     if ((threadIdx.x & 63) == 0) {
         if (w) atomicAdd(&R.cnt[ARTES_CNT_CROSSINGS], w);

@@ -252,27 +252,39 @@ static int32_t ensure_pool(artes_grid* g) {
     return 0;
 }
 
-template <bool G3D, int WPE, bool LDS>
+template <bool G3D, bool OBL, int WPE, bool LDS>
 static void launch_trace(artes_grid* g, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
     const size_t lds = LDS ? face_table_bytes(G.nr, G.ntheta, G.nphi) : 0;
     int per_cu = 0;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, WPE, LDS>, BLOCK, lds);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, OBL, WPE, LDS>, BLOCK, lds);
+    const char* bp = getenv("ARTES_TRACE_BPC");   // blocks per CU override (tuning)
+    if (bp) per_cu = atoi(bp);
     g->trace_blocks = std::max(1, per_cu) * g->num_cus;
     timed(g, ARTES_K_TRACE, stream, [&] {
-        hipLaunchKernelGGL((k_trace<G3D, WPE, LDS>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, LDS>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
 }
 
+template <bool G3D, bool OBL>
+static void launch_trace_lds(artes_grid* g, int wpe, bool lds, const DevGrid& G, const DevRun& R, const Lists& L,
+                             hipStream_t stream) {
+    if (lds) {
+        if (wpe == 5) launch_trace<G3D, OBL, 5, true>(g, G, R, L, stream);
+        else launch_trace<G3D, OBL, 4, true>(g, G, R, L, stream);
+    } else {
+        if (wpe == 5) launch_trace<G3D, OBL, 5, false>(g, G, R, L, stream);
+        else launch_trace<G3D, OBL, 4, false>(g, G, R, L, stream);
+    }
+}
+
+// k_trace variant: 3D or radial-only grid, spheroidal (oblate) or spherical planet,
+// occupancy target and face tables in LDS or global memory
 template <bool G3D>
 static void launch_trace_any(artes_grid* g, int wpe, bool lds, const DevGrid& G, const DevRun& R, const Lists& L,
                              hipStream_t stream) {
-    if (lds) {
-        if (wpe == 5) launch_trace<G3D, 5, true>(g, G, R, L, stream);
-        else launch_trace<G3D, 4, true>(g, G, R, L, stream);
-    } else {
-        if (wpe == 5) launch_trace<G3D, 5, false>(g, G, R, L, stream);
-        else launch_trace<G3D, 4, false>(g, G, R, L, stream);
-    }
+    const bool oblate = !(G.ax2 == 1.0 && G.by2 == 1.0 && G.cz2 == 1.0 && G.a == 1.0 && G.b == 1.0);
+    if (oblate) launch_trace_lds<G3D, true>(g, wpe, lds, G, R, L, stream);
+    else launch_trace_lds<G3D, false>(g, wpe, lds, G, R, L, stream);
 }
 
 template <bool G3D>

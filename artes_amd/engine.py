@@ -15,7 +15,7 @@ import numpy as np
 from .abi import ARTES_NUM_COUNTERS, ARTES_NUM_ERR, COUNTER_NAMES, GridArrays, GridDesc, RunParams
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libartes_hip.so")
+LIB_PATH = os.environ.get("ARTES_LIB_PATH") or os.path.join(HERE, "lib", "libartes_hip.so")
 
 _lib = None
 

@@ -1,0 +1,104 @@
+"""GPU engine plumbing: both engines (event, persistent) against each other and the
+oracle, per-launch timing hooks, launch-knob invariance, C-ABI argument checks."""
+
+import os
+
+import numpy as np
+import pytest
+
+from artes_amd import driver, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(name="ray3d", **spec):
+    from artes_amd.engine import Grid
+
+    atm = synthetic.make_config(name, **spec)
+    cfg = driver.default_config()
+    det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
+    grid = Grid(atm, device=0)
+    p = driver.run_params(cfg, det, 0, cell_depth=grid.cell_depth(0))
+    return atm, grid, p
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_event_and_persistent_engines_agree(require_gpu):
+    atm, grid, p = _setup(nr=8, ntheta=8, nphi=8)
+    ev = grid.trace(p, 0, 20000, 4242)
+    with _env(ARTES_ENGINE="persistent"):
+        pe = grid.trace(p, 0, 20000, 4242)
+    same = (np.isclose(ev[:, 0], pe[:, 0], rtol=1e-9, atol=1e-300) & (ev[:, 1] == pe[:, 1])
+            & (ev[:, 2] == pe[:, 2]) & (ev[:, 3] == pe[:, 3]))
+    assert same.mean() >= 0.999
+
+
+@pytest.mark.parametrize("knobs", [dict(ARTES_POOL="5000"), dict(ARTES_REFILL="1", ARTES_STATIC="0"),
+                                   dict(ARTES_REFILL="64", ARTES_STATIC="64"), dict(ARTES_LDS="0", ARTES_WPE="4")])
+def test_launch_knobs_do_not_change_results(require_gpu, knobs):
+    """Pool size, refill policy, trace-list split, LDS staging and occupancy only change
+    the schedule: per-packet histories and all counters are identical."""
+    atm, grid, p = _setup("hg")
+    base = grid.run(p, 0, 300000, 99)
+    grid.close()
+    with _env(**knobs):
+        atm, grid, p = _setup("hg")
+        other = grid.run(p, 0, 300000, 99)
+    np.testing.assert_array_equal(base.counters, other.counters)
+    np.testing.assert_allclose(base.det, other.det, rtol=1e-9, atol=1e-300)
+    np.testing.assert_allclose(base.totals, other.totals, rtol=1e-9)
+
+
+def test_kernel_times_profiling(require_gpu):
+    atm, grid, p = _setup()
+    assert grid.kernel_times()["trace"] == (0.0, 0)          # profiling off: nothing recorded
+    grid.set_profiling(True)
+    grid.run(p, 0, 10**6, 1)
+    kt = grid.kernel_times()
+    assert kt["trace"][1] >= 2 and kt["trace"][0] > 0.0
+    assert kt["event"][1] == kt["trace"][1] and kt["emit"][1] == kt["trace"][1] + 1
+    total = sum(ms for ms, _ in kt.values())
+    assert total <= grid.last_kernel_ms() * 1.05 + 0.5
+    assert grid.kernel_times()["trace"] == (0.0, 0)          # reset after reading
+    with _env(ARTES_ENGINE="persistent"):
+        grid.run(p, 0, 10**5, 1)
+    kt = grid.kernel_times()
+    assert kt["persistent"][1] == 1 and kt["trace"][1] == 0
+
+
+def test_unsupported_options_fail_loudly(require_gpu):
+    from artes_amd.engine import EngineError
+
+    atm, grid, p = _setup(nr=4, ntheta=4, nphi=4)
+    p.photon_source = 2
+    with pytest.raises(EngineError, match="planet"):
+        grid.run(p, 0, 10, 1)
+    p.photon_source = 1
+    p.wl_index = 3
+    with pytest.raises(EngineError, match="wl_index"):
+        grid.run(p, 0, 10, 1)
+
+
+def test_zero_and_tiny_runs(require_gpu):
+    atm, grid, p = _setup("iso")
+    r0 = grid.run(p, 0, 0, 1)
+    assert r0.det.sum() == 0.0 and r0.counters.sum() == 0
+    r1 = grid.run(p, 0, 1, 1)
+    assert r1.counter("packets") == 1
+    r7 = grid.run(p, 5, 7, 1)
+    assert r7.counter("packets") == 7
