@@ -25,6 +25,8 @@
 // the trace list is empty.
 #pragma once
 
+#include <cstddef>
+
 #include "device_common.hpp"
 
 namespace artes {
@@ -32,26 +34,31 @@ namespace artes {
 // packet-state pool: one 256-byte record per slot (two 128-byte cache lines).  The
 // work lists visit slots in no particular order, so a record layout keeps every access
 // of a lane inside its own two lines; a structure-of-arrays pool would touch one line per
-// field per lane.  Line 0 holds what k_trace needs, line 1 the event-only state.
+// field per lane.  Line 0 holds what k_trace reads and writes, line 1 the event-only
+// state.  Every trace starts at the packet position (p*, pcell, pface) with zero
+// accumulated optical depth, so no separate trace position is stored.
 struct alignas(256) Slot {
     // line 0: trace state
-    double tx, ty, tz, tacc, ttgt;      // trace position, accumulated / target optical depth
-    double dx, dy, dz;                  // packet direction
-    int tcell, tface;                   // trace cell / entry face (packed)
-    int mode, ncross;
-    unsigned long long r0, r1;          // xoroshiro128++ state
     double px, py, pz;                  // packet position (last interaction / emission)
-    int pcell, pface;
+    double dx, dy, dz;                  // packet direction
+    double ttgt;                        // target optical depth of a propagation trace
+    unsigned long long r0, r1;          // xoroshiro128++ state
+    int pcell, pface;                   // packed cell / face of the packet position
+    int mode, ncross;
+    double wI;                          // Stokes I including the weights applied in k_trace
+    double tpeel;                       // optical depth of the last peel-off trace
+    double spare0[3];
     // line 1: event state
-    double s0, s1, s2, s3;              // Stokes vector
+    double s0, s1, s2, s3;              // Stokes vector as of the last scattering
     double cs0, cs1, cs2, cs3;          // running contribution to the current pixel
     double pt0, pt1, pt2, pt3;          // packet total per Stokes
     double peel_sum;                    // trace records: total peeled intensity
     unsigned long long pid;
     int cur_pix, nscat;
-    double spare;
+    double spare1;
 };
 static_assert(sizeof(Slot) == 256, "slot record must be two cache lines");
+static_assert(offsetof(Slot, s0) == 128, "event state must start the second line");
 
 struct Pool {
     int P;
@@ -180,214 +187,8 @@ struct WaveQueue {
     }
 };
 
-// bytes of LDS holding the per-coordinate face tables (rf2, thetaf, tan2, phis, phic, tplane)
-__host__ __device__ inline size_t face_table_bytes(int nr, int ntheta, int nphi) {
-    return sizeof(double) * ((size_t)(nr + 1) + 2 * (size_t)(ntheta + 1) + 2 * (size_t)nphi) + sizeof(int) * (size_t)(ntheta + 1);
-}
-
-// stage the face tables in LDS: every trace step reads ~12 of them at indices that depend
-// on the previous step, so their latency is on the critical path; LDS answers in ~64
-// cycles where an L2 hit takes ~200-500
-__device__ __forceinline__ DevGrid stage_face_tables(const DevGrid& G, double* lds) {
-    DevGrid GL = G;
-    double* p = lds;
-    auto copy = [&](const double* src, int cnt) {
-        for (int i = threadIdx.x; i < cnt; i += BLOCK) p[i] = src[i];
-        double* out = p;
-        p += cnt;
-        return out;
-    };
-    GL.rf2 = copy(G.rf2, G.nr + 1);
-    GL.thetaf = copy(G.thetaf, G.ntheta + 1);
-    GL.tan2 = copy(G.tan2, G.ntheta + 1);
-    GL.phis = copy(G.phis, G.nphi);
-    GL.phic = copy(G.phic, G.nphi);
-    int* ip = (int*)p;
-    for (int i = threadIdx.x; i < G.ntheta + 1; i += BLOCK) ip[i] = G.tplane[i];
-    GL.tplane = ip;
-    __syncthreads();
-    return GL;
-}
-
-template <bool G3D, bool OBL, int WPE, bool LDS>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G0, DevRun R, Pool S, Lists L) {
-    extern __shared__ double s_tab[];
-    const DevGrid G = LDS ? stage_face_tables(G0, s_tab) : G0;
-    const int n = *L.trace_in_n;
-    const int home = blockIdx.x & 7;
-    __shared__ int s_q[2][BLOCK];
-    const int wbase = threadIdx.x & ~63;
-    WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
-    TraceCursor cur = make_cursor(n, R.static_q64);
-    bool have = false;
-#ifdef ARTES_DEBUG_LANES
-    unsigned long long dbg_steps = 0, dbg_lanes = 0, dbg_refills = 0;
-#endif
-    int slot = -1, mode = 0, tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0;
-    double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, ttgt = 0;
-    uint32_t c_cross = 0, c_peel = 0, seg_cross = 0;
-
-    for (;;) {
-        // ---------------------------------------------------------------- refill
-        if (!cur.exhausted) {
-            const unsigned long long idle = __ballot(!have);
-            if (__popcll(idle) >= R.refill || idle == __ballot(true)) {
-                const int my = wave_take(cur, L.grab, home, !have);
-#ifdef ARTES_DEBUG_LANES
-                dbg_refills++;
-#endif
-                if (!have && my >= 0) {
-                    slot = L.trace_in[my];
-                    mode = S.s[slot].mode;
-                    tx = S.s[slot].tx; ty = S.s[slot].ty; tz = S.s[slot].tz;
-                    tacc = S.s[slot].tacc; ttgt = S.s[slot].ttgt;
-                    unpack_cell(S.s[slot].tcell, tcr, tct, tcp);
-                    unpack_face(S.s[slot].tface, tft, tfi);
-                    // load the direction unconditionally (one round trip with the rest of the record)
-                    const double ldx = S.s[slot].dx, ldy = S.s[slot].dy, ldz = S.s[slot].dz;
-                    const bool peel = (mode == S_PEEL);
-                    nx = peel ? R.det0 : ldx; ny = peel ? R.det1 : ldy; nz = peel ? R.det2 : ldz;
-                    seg_cross = 0;
-                    have = true;
-                }
-            }
-        }
-        if (!__any(have)) break;
-#ifdef ARTES_DEBUG_LANES
-        dbg_steps++;
-        dbg_lanes += __popcll(__ballot(have));
-#endif
-        int end = 0;   // 0: continue, else the slot's new mode
-        if (have) {
-        // ------------------------------------------------------------ trace step
-        Step o;
-        cell_face<G3D, OBL>(G, R, tx, ty, tz, nx, ny, nz, tft, tfi, tcr, tct, tcp, o);
-        c_cross++;
-        seg_cross++;
-        const double k = G.kappa[tcr + G.nr * (tct + G.ntheta * tcp)];
-#ifdef ARTES_DEBUG_LANES
-        // timing probe: extra dependent FP64 work per step (R.defer iterations; result unused but kept)
-        double spin = o.d;
-        for (int q = 0; q < R.defer; q += 16) {
-#pragma unroll
-            for (int u = 0; u < 16; u++) spin = fma(spin, 1.0000001, 1e-30);
-        }
-        if (spin == 12345.678) log_err(R, 58);
-#endif
-        const double tau_cell = o.d * k;
-        const bool surf = (o.nft == 1 && o.nfi == G.cell_depth);
-        const bool prop = (mode == S_PROP);
-        // common case for every trace kind: no interaction in this cell, no boundary event
-        const bool stop = o.err || o.exit || surf || (prop && tacc + tau_cell > ttgt);
-        if (!stop) {
-            tacc += tau_cell;
-            tx += o.d * nx; ty += o.d * ny; tz += o.d * nz;
-            tft = o.nft; tfi = o.nfi; tcr = o.ncr; tct = o.nct; tcp = o.ncp;
-        } else if (prop) {
-            if (o.err) {
-                log_err(R, 3);
-                end = S_END_DROP;
-            } else if (tacc + tau_cell > ttgt) {          // interaction in this cell (ARTES.f90:705-720)
-                const double s = (ttgt - tacc) / k;
-                const double px = tx + s * nx, py = ty + s * ny, pz = tz + s * nz;
-                S.s[slot].px = px; S.s[slot].py = py; S.s[slot].pz = pz;
-                S.s[slot].pcell = pack_cell(tcr, tct, tcp);
-                S.s[slot].pface = 0;
-                // scattering-loop head (ARTES.f90:788-813)
-                Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
-                bool kill = !R.photon_scattering;
-                if (!kill) kill = rng.uni() < R.fstop;
-                if (!kill) {
-                    const double alb = G.albedo[tcr + G.nr * (tct + G.ntheta * tcp)];
-                    if (alb < 1.0 && alb > 0.0) {
-                        const double gamma = alb / (1.0 - R.fstop);
-                        S.s[slot].s0 *= gamma; S.s[slot].s1 *= gamma; S.s[slot].s2 *= gamma; S.s[slot].s3 *= gamma;
-                    }
-                    if (S.s[slot].s0 <= R.pmin) kill = true;
-                }
-                S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
-                if (kill) {
-                    end = S_END_ABS;
-                } else {                                   // peel-off trace (ARTES.f90:4722-4761)
-                    c_peel++;
-                    tx = px; ty = py; tz = pz;
-                    nx = R.det0; ny = R.det1; nz = R.det2;
-                    tft = 0; tfi = 0;
-                    tacc = 0.0;
-                    mode = S_PEEL;
-                }
-            } else if (o.exit) {                           // left the atmosphere
-                end = S_END_EXIT;
-            } else {                                       // reached the surface (ARTES.f90:755-774)
-                Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
-                const double xi = rng.uni();
-                S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
-                if (xi > R.surface_albedo) end = S_END_ABS;
-                else { log_err(R, 62); end = S_END_DROP; }
-            }
-        } else {   // S_FIRST or S_PEEL reached the boundary: total optical depth known
-            tacc += tau_cell;
-            if (o.err) log_err(R, mode == S_FIRST ? 2 : 43);
-            if (mode == S_PEEL) {
-                S.s[slot].tacc = tacc;
-                end = S_PEEL_DONE | (o.exit ? FLAG_EXIT : 0) | (o.err ? FLAG_ERR : 0);
-            } else {   // forced first interaction (ARTES.f90:658-685)
-                const double tau_first = tacc;
-                if (tau_first < 1.e-6 && !surf) {
-                    end = S_END_DROP;
-                } else {
-                    Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
-                    const double xi = rng.uni();
-                    double tau;
-                    if (tau_first < 1.e-6) {
-                        tau = -log(1.0 - xi);
-                    } else if (tau_first < 50.0) {
-                        const double e = 1.0 - exp(-tau_first);
-                        tau = -log(1.0 - xi * e);
-                        S.s[slot].s0 *= e; S.s[slot].s1 *= e; S.s[slot].s2 *= e; S.s[slot].s3 *= e;
-                    } else {
-                        tau = -log(1.0 - xi);
-                    }
-                    S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
-                    tx = S.s[slot].px; ty = S.s[slot].py; tz = S.s[slot].pz;
-                    unpack_cell(S.s[slot].pcell, tcr, tct, tcp);
-                    unpack_face(S.s[slot].pface, tft, tfi);
-                    tacc = 0.0; ttgt = tau;
-                    mode = S_PROP;
-                }
-            }
-        }
-        if (end) {
-            S.s[slot].mode = end;
-            S.s[slot].ncross += seg_cross;
-            have = false;
-        }
-        }   // have
-        q_event.push(end && (end & 0xFF) == S_PEEL_DONE, slot, L.event, L.event_n);
-        q_emit.push(end && (end & 0xFF) != S_PEEL_DONE, slot, L.emit, L.emit_n);
-    }
-    q_event.flush(L.event, L.event_n);
-    q_emit.flush(L.emit, L.emit_n);
-#ifdef ARTES_DEBUG_LANES
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&R.err[60], dbg_steps);
-        atomicAdd(&R.err[61], dbg_lanes);
-        atomicAdd(&R.err[59], dbg_refills);
-    }
-#endif
-    const unsigned long long w = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);
-    if ((threadIdx.x & 63) == 0) {
-        if (w) atomicAdd(&R.cnt[ARTES_CNT_CROSSINGS], w);
-        if (wp) atomicAdd(&R.cnt[ARTES_CNT_PEELS], wp);
-    }
-}
-
 // park the packet in a new propagation trace starting at its position
 __device__ __forceinline__ void start_prop(const Pool& S, int slot, double tau) {
-    S.s[slot].tx = S.s[slot].px; S.s[slot].ty = S.s[slot].py; S.s[slot].tz = S.s[slot].pz;
-    S.s[slot].tcell = S.s[slot].pcell;
-    S.s[slot].tface = S.s[slot].pface;
-    S.s[slot].tacc = 0.0;
     S.s[slot].ttgt = tau;
     S.s[slot].mode = S_PROP;
 }
@@ -400,13 +201,17 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         if (m & FLAG_ERR) { S.s[slot].mode = S_END_DROP; return 2; }
         const double px = S.s[slot].px, py = S.s[slot].py, pz = S.s[slot].pz;
         double dx = S.s[slot].dx, dy = S.s[slot].dy, dz = S.s[slot].dz;
-        double st[4] = {S.s[slot].s0, S.s[slot].s1, S.s[slot].s2, S.s[slot].s3};
+        // k_trace scaled I by the forced-first-interaction and albedo weights (ARTES.f90:
+        // 674-676, 801-807); the polarised components follow by the same factor
+        const double wI = S.s[slot].wI, sI = S.s[slot].s0;
+        const double f = (wI != sI && sI != 0.0) ? wI / sI : 1.0;
+        double st[4] = {wI, S.s[slot].s1 * f, S.s[slot].s2 * f, S.s[slot].s3 * f};
         int cr, ct, cp;
         unpack_cell(S.s[slot].pcell, cr, ct, cp);
         const int cell = cr + G.nr * (ct + G.ntheta * cp);
         const int mid = G.matid[cell];
         const double* __restrict__ P = G.mats + (size_t)mid * MAT_DOUBLES;
-        const double tau_peel = S.s[slot].tacc;
+        const double tau_peel = S.s[slot].tpeel;
         bool drop = false;
         if ((m & FLAG_EXIT) && tau_peel < 50.0) {
             const double w = exp(-tau_peel);
@@ -497,6 +302,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             double sn[4];
             polarization_rotation(R, alpha, beta, st, sc, dz, e2, sn, false);
             S.s[slot].s0 = sn[0]; S.s[slot].s1 = sn[1]; S.s[slot].s2 = sn[2]; S.s[slot].s3 = sn[3];
+            S.s[slot].wI = sn[0];
             S.s[slot].dx = e0; S.s[slot].dy = e1; S.s[slot].dz = e2;
             const double xi = rng.uni();
             S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
@@ -628,11 +434,9 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         S.s[slot].px = px; S.s[slot].py = py; S.s[slot].pz = pz;
         S.s[slot].dx = dx; S.s[slot].dy = dy; S.s[slot].dz = dz;
         S.s[slot].s0 = 1.0; S.s[slot].s1 = 0.0; S.s[slot].s2 = 0.0; S.s[slot].s3 = 0.0;
-        const int pc = pack_cell(cr, ct, cp), pf = pack_face(1, G.nr);
-        S.s[slot].pcell = pc; S.s[slot].pface = pf;
-        S.s[slot].tx = px; S.s[slot].ty = py; S.s[slot].tz = pz;
-        S.s[slot].tcell = pc; S.s[slot].tface = pf;
-        S.s[slot].tacc = 0.0; S.s[slot].ttgt = 0.0;
+        S.s[slot].wI = 1.0;
+        S.s[slot].pcell = pack_cell(cr, ct, cp); S.s[slot].pface = pack_face(1, G.nr);
+        S.s[slot].ttgt = 0.0;
         S.s[slot].cs0 = S.s[slot].cs1 = S.s[slot].cs2 = S.s[slot].cs3 = 0.0;
         S.s[slot].pt0 = S.s[slot].pt1 = S.s[slot].pt2 = S.s[slot].pt3 = 0.0;
         S.s[slot].peel_sum = 0.0;

@@ -1,0 +1,409 @@
+// kernel_trace.hpp -- k_trace, the hot loop of the event engine.
+//
+// Every trace of the reference -- first optical depth (ARTES.f90:625-656), propagation
+// (689-778, 848-941) and peel-off (4739-4761) -- is a sequence of cell_face calls
+// (2800-3470): from the current position, the distance to every face of the current
+// cell (inner/outer sphere, inner/outer theta cone or the 90-degree plane, the two phi
+// half-planes) and the nearest one wins.
+//
+// Along a straight trace the faces of a coordinate family do not change until the trace
+// crosses a face of THAT family: crossing a phi face leaves the cell's radial shell and
+// theta band, so their candidate crossings are still the ones found before.  This
+// kernel therefore keeps the six candidates (as trace parameters t) in registers and,
+// after each crossing, re-evaluates only the family that was crossed -- with the
+// reference's own formulas, tolerances and same-face rules, from the current position.
+// That is one pair of quadratics (spheres or cones) or one pair of plane intersections
+// per step instead of four quadratics and three plane intersections.  The family to
+// evaluate differs from lane to lane, so the evaluation is written once for all three
+// (coefficients and operands are selected per lane, the arithmetic is shared): the wave
+// executes one evaluation per step, not three.  A new trace evaluates its families one
+// per step before it moves (radial, theta, phi), so set-up costs two extra steps and no
+// divergent branch.
+//
+// Divisions and square roots use reciprocal / reciprocal-square-root seeds refined by
+// Newton steps (<= 1-2 ulp); the reference's correctly rounded forms cost twice the VALU
+// work, and the trajectory parity tests (tests/test_gpu_parity.py) bound the effect.
+#pragma once
+
+#include "device_common.hpp"
+
+namespace artes {
+
+// ------------------------------------------------------------ fast math ---
+// a / b to ~1 ulp for normal operands (b = 0 gives inf/nan: callers select it away)
+__device__ __forceinline__ double fast_div(double a, double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    const double q = a * r;
+    return fma(fma(-b, q, a), r, q);
+}
+__device__ __forceinline__ double fast_rcp(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    return fma(fma(-b, r, 1.0), r, r);
+}
+// sqrt(x) to ~1 ulp for x > 0 (x <= 0 gives 0)
+__device__ __forceinline__ double fast_sqrt(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-g, h, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    const double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return x > 0.0 ? g : 0.0;
+}
+
+// ---------------------------------------------------- face tables (LDS) ---
+// fv[0..nr] = rfront^2, fv[nr+1 .. nr+1+ntheta] = tan^2(theta_f): one array so the
+// radial and theta families read their two face values with the same instruction;
+// tfl[k] = theta-face flags; phsc[2k], phsc[2k+1] = sin, cos(phi_k)
+constexpr int TF_CONE = 1, TF_GT90 = 2, TF_LT90 = 4;
+
+struct TraceTabs {
+    const double* fv;
+    const double* phsc;
+    const int* tfl;
+};
+
+__host__ __device__ inline size_t trace_table_bytes(int nr, int ntheta, int nphi) {
+    return sizeof(double) * ((size_t)(nr + 1) + (size_t)(ntheta + 1) + 2 * (size_t)nphi) + sizeof(int) * (size_t)(ntheta + 1);
+}
+
+__device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double* lds) {
+    TraceTabs T;
+    double* fv = lds;
+    for (int i = threadIdx.x; i <= G.nr; i += BLOCK) fv[i] = G.rf2[i];
+    for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) fv[G.nr + 1 + i] = G.tan2[i];
+    double* phsc = fv + (G.nr + 1) + (G.ntheta + 1);
+    for (int i = threadIdx.x; i < G.nphi; i += BLOCK) { phsc[2 * i] = G.phis[i]; phsc[2 * i + 1] = G.phic[i]; }
+    int* tfl = (int*)(phsc + 2 * G.nphi);
+    for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) {
+        const double th = G.thetaf[i];
+        tfl[i] = (G.tplane[i] == 1 ? TF_CONE : 0) | (th > HALF_PI ? TF_GT90 : 0) | (th < HALF_PI ? TF_LT90 : 0);
+    }
+    __syncthreads();
+    T.fv = fv; T.phsc = phsc; T.tfl = tfl;
+    return T;
+}
+
+// ------------------------------------------------------- family evaluation ---
+// Candidate distances to the inner and outer face of ONE coordinate family of cell
+// (cr, ct, cp) from (x, y, z) along n, for a packet sitting on face (ft, fi):
+//   fam 0: spheres r_cr, r_cr+1   (ARTES.f90:2885-3010)
+//   fam 1: theta cones / the 90-degree plane, faces ct, ct+1 (3014-3290)
+//   fam 2: phi half-planes cp, cp+1 (3292-3350)
+// 0 = no candidate, as in the reference.  zp = distance to the plane z = 0.
+template <bool G3D, bool OBL>
+__device__ __forceinline__ void family_candidates(const DevGrid& G, const TraceTabs& T, int fam, double x, double y,
+                                                  double z, double n0, double n1, double n2, int ft, int fi, int cr,
+                                                  int ct, int cp, double zp, double& d_in, double& d_out) {
+    const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
+    const bool isR = !G3D || fam == 0;
+    const bool isT = G3D && fam == 1;
+    const bool isP = G3D && fam == 2;
+    // sphere:  ax2 x^2 + by2 y^2 + cz2 z^2 - r^2        (w = 1,       off = r^2)
+    // cone:    ax2 x^2 + by2 y^2 - cz2 z^2 tan^2(theta) (w = -tan^2, off = 0)
+    const double Axy = ax2 * n0 * n0 + by2 * n1 * n1, Az = cz2 * n2 * n2;
+    const double Bxy = ax2 * x * n0 + by2 * y * n1, Bz = cz2 * z * n2;
+    const double Cxy = ax2 * x * x + by2 * y * y, Cz = cz2 * z * z;
+    const int kin = isR ? cr : ct;
+    const int vb = isR ? 0 : G.nr + 1;
+    const double vin = T.fv[vb + kin], vout = T.fv[vb + kin + 1];
+    const double win = isR ? 1.0 : -vin, wout = isR ? 1.0 : -vout;
+    const double qa0 = Axy + win * Az, qb0 = 2.0 * (Bxy + win * Bz), qc0 = Cxy + win * Cz - (isR ? vin : 0.0);
+    const double qa1 = Axy + wout * Az, qb1 = 2.0 * (Bxy + wout * Bz), qc1 = Cxy + wout * Cz - (isR ? vout : 0.0);
+    // quadratic_equation (ARTES.f90:4154-4173), both faces
+    const double disc0 = qb0 * qb0 - 4.0 * qa0 * qc0, disc1 = qb1 * qb1 - 4.0 * qa1 * qc1;
+    const double q0 = -0.5 * (qb0 + copysign(fast_sqrt(disc0), qb0));
+    const double q1 = -0.5 * (qb1 + copysign(fast_sqrt(disc1), qb1));
+    // phi half-planes: num / den per face (ARTES.f90:3300-3346)
+    double num0 = 0.0, den0 = 1.0, num1 = 0.0, den1 = 1.0;
+    int pout = 0;
+    if constexpr (G3D) {
+        const double ga = OBL ? G.a : 1.0, gb = OBL ? G.b : 1.0;
+        pout = (cp + 1 == G.nphi) ? 0 : cp + 1;
+        const double s0 = T.phsc[2 * cp], c0 = T.phsc[2 * cp + 1];
+        const double s1 = T.phsc[2 * pout], c1 = T.phsc[2 * pout + 1];
+        den0 = gb * n1 * c0 - ga * n0 * s0; num0 = ga * x * s0 - gb * y * c0;
+        den1 = gb * n1 * c1 - ga * n0 * s1; num1 = ga * x * s1 - gb * y * c1;
+    }
+    // four divisions shared by the families: quadratic roots q/a and c/q, or the two
+    // plane intersections num/den
+    const double ra0 = fast_div(isP ? num0 : q0, isP ? den0 : qa0);
+    const double rb0 = fast_div(qc0, q0);
+    const double ra1 = fast_div(isP ? num1 : q1, isP ? den1 : qa1);
+    const double rb1 = fast_div(qc1, q1);
+    if (isP) {
+        const bool on_p = (ft == 3);
+        const double sp0 = (!(on_p && fi == cp) && fabs(den0) > 0.0) ? ra0 : 0.0;
+        d_in = (sp0 > 1.e-15 && sp0 < 1.e100) ? sp0 : 0.0;
+        const bool ok1 = !(on_p && fi == pout) && fabs(den1) > 0.0;
+        d_out = (ok1 && ra1 > 1.e-15 && sp0 < 1.e100) ? ra1 : 0.0;   // sic: sp0 (ARTES.f90:3318, 3346)
+        return;
+    }
+    const bool ok0 = disc0 >= 0.0, ok1 = disc1 >= 0.0;
+    double s00 = (ok0 && fabs(qa0) > 1.e-100) ? ra0 : 0.0, s01 = (ok0 && fabs(q0) > 1.e-100) ? rb0 : 0.0;
+    double s10 = (ok1 && fabs(qa1) > 1.e-100) ? ra1 : 0.0, s11 = (ok1 && fabs(q1) > 1.e-100) ? rb1 : 0.0;
+    const int kout = kin + 1;
+    const int fl0 = isT ? T.tfl[kin] : 0, fl1 = isT ? T.tfl[kout] : 0;
+    if (isT) {   // nappe filter (ARTES.f90:3040-3064)
+        auto wrong = [&](double s, int fl) {
+            const double zz = z + s * n2;
+            return s > 1.e-15 && ((zz > 0.0 && (fl & TF_GT90)) || (zz < 0.0 && (fl & TF_LT90)));
+        };
+        if (wrong(s00, fl0)) s00 = 0.0;
+        if (wrong(s01, fl0)) s01 = 0.0;
+        if (wrong(s10, fl1)) s10 = 0.0;
+        if (wrong(s11, fl1)) s11 = 0.0;
+    }
+    const int ftype = isR ? 1 : 2;
+    const bool same0 = (ft == ftype && fi == kin), same1 = (ft == ftype && fi == kout);
+    const double p0 = pick_root(s00, s01, (same0 && isT) ? 1.e-3 : 1.e-15);
+    const double p1 = pick_root(s10, s11, same1 ? 1.e-3 : 1.e-15);
+    if (isR) {
+        d_in = same0 ? 0.0 : p0;
+        d_out = p1;
+    } else {
+        double a, b;
+        if (fl0 & TF_CONE) a = (!same0 || (fl0 & TF_GT90)) ? p0 : 0.0;
+        else a = (!same0 && zp > 0.0 && n2 > 1.e-15) ? zp : 0.0;
+        if (fl1 & TF_CONE) b = (!same1 || (fl1 & TF_LT90)) ? p1 : 0.0;
+        else b = (!same1 && zp > 0.0 && n2 < -1.e-15) ? zp : 0.0;
+        d_in = (ct != 0) ? a : 0.0;
+        d_out = (kout != G.ntheta) ? b : 0.0;
+    }
+}
+
+// -------------------------------------------------------------- k_trace ---
+// A lane takes a slot from the trace list and runs its traces back to back as long as
+// they chain inside the reference's packet loop: first optical depth -> propagation
+// (forced first interaction, ARTES.f90:658-685) -> peel-off (scattering-loop head,
+// 788-813) -> k_event.  Everything a chain needs is loaded once at refill and kept in
+// registers (position, direction, RNG state, Stokes I); the slot is written back once
+// when the chain ends, so no transition waits on memory.
+template <bool G3D, bool OBL, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G, DevRun R, Pool S, Lists L) {
+    extern __shared__ double s_tab[];
+    const TraceTabs T = stage_trace_tables(G, s_tab);
+    const int n = *L.trace_in_n;
+    const int home = blockIdx.x & 7;
+    __shared__ int s_q[2][BLOCK];
+    const int wbase = threadIdx.x & ~63;
+    WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
+    TraceCursor cur = make_cursor(n, R.static_q64);
+    const int fam_all = !G3D ? 1 : (G.nphi > 1 ? 7 : 3);
+    constexpr double NONE = -1.e300;
+    bool have = false;
+#ifdef ARTES_DEBUG_LANES
+    unsigned long long dbg_steps = 0, dbg_lanes = 0, dbg_refills = 0, dbg_tsteps = 0, dbg_tlanes = 0;
+#endif
+    // packet state (slot line 0) and trace state
+    int slot = -1, mode = 0, pcell = 0, pface = 0, ncross = 0;
+    double px = 0, py = 0, pz = 0, ttgt = 0, wI = 0;
+    Rng rng{0, 0};
+    int tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0, pending = 0;
+    double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, tpar = 0, inz = 0;
+    // cached candidates as trace parameters: rin, tin, pin, rout, tout, pout
+    double c0 = NONE, c1 = NONE, c2 = NONE, c3 = NONE, c4 = NONE, c5 = NONE;
+    uint32_t c_cross = 0, c_peel = 0;
+
+    // a trace starts at the packet position with zero optical depth
+    auto start_trace = [&](double d0, double d1, double d2) {
+        tx = px; ty = py; tz = pz;
+        unpack_cell(pcell, tcr, tct, tcp);
+        unpack_face(pface, tft, tfi);
+        nx = d0; ny = d1; nz = d2;
+        tacc = 0.0;
+        tpar = 0.0;
+        pending = fam_all;
+        if constexpr (G3D) inz = fast_rcp(nz);
+    };
+
+    for (;;) {
+        // ---------------------------------------------------------------- refill
+        if (!cur.exhausted) {
+            const unsigned long long idle = __ballot(!have);
+            if (__popcll(idle) >= R.refill || idle == __ballot(true)) {
+                const int my = wave_take(cur, L.grab, home, !have);
+#ifdef ARTES_DEBUG_LANES
+                dbg_refills++;
+#endif
+                if (!have && my >= 0) {
+                    slot = L.trace_in[my];
+                    const Slot* rec = S.s + slot;
+                    mode = rec->mode;
+                    px = rec->px; py = rec->py; pz = rec->pz;
+                    const double ldx = rec->dx, ldy = rec->dy, ldz = rec->dz;
+                    ttgt = rec->ttgt;
+                    rng.s0 = rec->r0; rng.s1 = rec->r1;
+                    pcell = rec->pcell; pface = rec->pface;
+                    ncross = rec->ncross;
+                    wI = rec->wI;
+                    const bool peel = (mode == S_PEEL);
+                    start_trace(peel ? R.det0 : ldx, peel ? R.det1 : ldy, peel ? R.det2 : ldz);
+                    have = true;
+                }
+            }
+        }
+        if (!__any(have)) break;
+#ifdef ARTES_DEBUG_LANES
+        dbg_steps++;
+        dbg_lanes += __popcll(__ballot(have));
+        if (cur.exhausted) { dbg_tsteps++; dbg_tlanes += __popcll(__ballot(have)); }
+#endif
+        int end = 0;   // 0: continue, else the slot's new mode
+        if (have) {
+            // extinction and albedo of the current cell: issued first so the L2 round trip
+            // overlaps the face evaluation (the cell is known before the step)
+            const int cell = tcr + G.nr * (tct + G.ntheta * tcp);
+            const double k = G.kappa[cell];
+            const double alb = G.albedo[cell];
+            // ------------------------------------------- evaluate one face family
+            const int fam = G3D ? __builtin_ctz(pending) : 0;
+            double din, dout;
+            family_candidates<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, tft, tfi, tcr, tct, tcp, -tz * inz, din, dout);
+            const double tin = din > 0.0 ? tpar + din : NONE, tout = dout > 0.0 ? tpar + dout : NONE;
+            if (fam == 0) { c0 = tin; c3 = tout; }
+            if constexpr (G3D) {
+                if (fam == 1) { c1 = tin; c4 = tout; }
+                if (fam == 2) { c2 = tin; c5 = tout; }
+            }
+            pending &= pending - 1;
+            if (pending == 0) {
+                // ------------------------------------------------ trace step
+                // distances: exact for the family just evaluated, from the cache otherwise
+                const double e0 = fam == 0 ? din : c0 - tpar, e3 = fam == 0 ? dout : c3 - tpar;
+                double e1 = 0.0, e2 = 0.0, e4 = 0.0, e5 = 0.0;
+                if constexpr (G3D) {
+                    e1 = fam == 1 ? din : c1 - tpar; e4 = fam == 1 ? dout : c4 - tpar;
+                    e2 = fam == 2 ? din : c2 - tpar; e5 = fam == 2 ? dout : c5 - tpar;
+                }
+                // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
+                double best = 1.e100;
+                int which = -1;
+#define ARTES_CONSIDER(dd, w, thr) if ((dd) > (thr) && (dd) < best) { best = (dd); which = (w); }
+                ARTES_CONSIDER(e0, 0, 1.e-9)
+                if constexpr (G3D) { ARTES_CONSIDER(e1, 1, 1.e-9) ARTES_CONSIDER(e2, 2, 1.e-9) }
+                ARTES_CONSIDER(e3, 3, 1.e-9)
+                if constexpr (G3D) { ARTES_CONSIDER(e4, 4, 1.e-9) ARTES_CONSIDER(e5, 5, 1.e-9) }
+                if (which < 0) {
+                    best = 1.e100;
+                    ARTES_CONSIDER(e0, 0, 1.e-12)
+                    if constexpr (G3D) { ARTES_CONSIDER(e1, 1, 1.e-12) ARTES_CONSIDER(e2, 2, 1.e-12) }
+                    ARTES_CONSIDER(e3, 3, 1.e-12)
+                    if constexpr (G3D) { ARTES_CONSIDER(e4, 4, 1.e-12) ARTES_CONSIDER(e5, 5, 1.e-12) }
+                }
+#undef ARTES_CONSIDER
+                // next_cell (ARTES.f90:2671-2798)
+                int nft = 0, nfi = -999, ncr = tcr, nct = tct, ncp = tcp;
+                bool err = false;
+                switch (which) {
+                    case 0: nft = 1; nfi = tcr; ncr = tcr - 1; break;
+                    case 3: nft = 1; nfi = tcr + 1; ncr = tcr + 1; break;
+                    case 1: nft = 2; nfi = tct; nct = tct - 1; break;
+                    case 4: nft = 2; nfi = tct + 1; nct = tct + 1; break;
+                    case 2: nft = 3; nfi = tcp; ncp = (tcp == 0) ? G.nphi - 1 : tcp - 1; break;
+                    case 5: nft = 3; { const int po = (tcp + 1 == G.nphi) ? 0 : tcp + 1; nfi = po; ncp = po; } break;
+                    default: err = true; log_err(R, 31); break;
+                }
+                const bool exit = (nft == 1 && nfi == G.nr);
+                if (tft == 1 && tfi == G.cell_depth && nft == 1 && nfi == G.cell_depth) { err = true; log_err(R, 34); }
+                if (ncr < 0) ncr = 0;
+                c_cross++;
+                ncross++;
+                const double tau_cell = best * k;
+                const bool surf = (nft == 1 && nfi == G.cell_depth);
+                const bool prop = (mode == S_PROP);
+                const bool hit = prop && tacc + tau_cell > ttgt;
+                const bool stop = err || exit || surf || hit;
+                if (!stop) {
+                    tacc += tau_cell;
+                    tx += best * nx; ty += best * ny; tz += best * nz;
+                    tpar += best;
+                    tft = nft; tfi = nfi; tcr = ncr; tct = nct; tcp = ncp;
+                    pending = 1 << (which % 3);
+                } else if (prop && !err && hit) {
+                    // interaction in this cell (ARTES.f90:705-720), then the scattering-loop
+                    // head (788-813): roulette, albedo weight, minimum weight
+                    const double s = fast_div(ttgt - tacc, k);
+                    px = tx + s * nx; py = ty + s * ny; pz = tz + s * nz;
+                    pcell = pack_cell(tcr, tct, tcp);
+                    pface = 0;
+                    const double xi = rng.uni();   // a killed packet's RNG state is not used again
+                    bool kill = !R.photon_scattering || xi < R.fstop;
+                    if (alb < 1.0 && alb > 0.0) wI *= alb / (1.0 - R.fstop);
+                    kill = kill || wI <= R.pmin;
+                    if (kill) {
+                        end = S_END_ABS;
+                    } else {                                       // peel-off trace (ARTES.f90:4722-4761)
+                        c_peel++;
+                        mode = S_PEEL;
+                        start_trace(R.det0, R.det1, R.det2);
+                    }
+                } else if (prop) {
+                    if (err) {
+                        log_err(R, 3);
+                        end = S_END_DROP;
+                    } else if (exit) {                             // left the atmosphere
+                        end = S_END_EXIT;
+                    } else {                                       // reached the surface (ARTES.f90:755-774)
+                        const double xi = rng.uni();
+                        if (xi > R.surface_albedo) end = S_END_ABS;
+                        else { log_err(R, 62); end = S_END_DROP; }
+                    }
+                } else {   // S_FIRST or S_PEEL reached the boundary: total optical depth known
+                    tacc += tau_cell;
+                    if (err) log_err(R, mode == S_FIRST ? 2 : 43);
+                    if (mode == S_PEEL) {
+                        end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0);
+                    } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
+                        end = S_END_DROP;
+                    } else {
+                        // one exp and one log for every case: e = 1 outside [1e-6, 50)
+                        const double tau_first = tacc;
+                        const double xi = rng.uni();
+                        const bool mid = tau_first >= 1.e-6 && tau_first < 50.0;
+                        const double e = mid ? 1.0 - exp(-tau_first) : 1.0;
+                        const double tau = -log(1.0 - xi * e);
+                        if (mid) wI *= e;
+                        ttgt = tau;
+                        mode = S_PROP;
+                        start_trace(nx, ny, nz);
+                    }
+                }
+                if (end) {   // write the packet state back once
+                    Slot* rec = S.s + slot;
+                    rec->px = px; rec->py = py; rec->pz = pz;
+                    rec->r0 = rng.s0; rec->r1 = rng.s1;
+                    rec->pcell = pcell; rec->pface = pface;
+                    rec->mode = end; rec->ncross = ncross;
+                    rec->wI = wI;
+                    rec->tpeel = tacc;
+                    have = false;
+                }
+            }   // pending == 0
+        }   // have
+        q_event.push(end && (end & 0xFF) == S_PEEL_DONE, slot, L.event, L.event_n);
+        q_emit.push(end && (end & 0xFF) != S_PEEL_DONE, slot, L.emit, L.emit_n);
+    }
+    q_event.flush(L.event, L.event_n);
+    q_emit.flush(L.emit, L.emit_n);
+#ifdef ARTES_DEBUG_LANES
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&R.err[60], dbg_steps);
+        atomicAdd(&R.err[61], dbg_lanes);
+        atomicAdd(&R.err[59], dbg_refills);
+        atomicAdd(&R.err[54], dbg_tsteps);
+        atomicAdd(&R.err[55], dbg_tlanes);
+    }
+#endif
+    const unsigned long long w = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);
+    if ((threadIdx.x & 63) == 0) {
+        if (w) atomicAdd(&R.cnt[ARTES_CNT_CROSSINGS], w);
+        if (wp) atomicAdd(&R.cnt[ARTES_CNT_PEELS], wp);
+    }
+}
+
+}  // namespace artes

@@ -29,6 +29,7 @@
 #include "device_common.hpp"
 #include "kernel_persistent.hpp"
 #include "kernel_event.hpp"
+#include "kernel_trace.hpp"
 
 namespace artes {
 
@@ -252,39 +253,32 @@ static int32_t ensure_pool(artes_grid* g) {
     return 0;
 }
 
-template <bool G3D, bool OBL, int WPE, bool LDS>
+// k_trace (kernel_trace.hpp) with its face tables in LDS
+template <bool G3D, bool OBL, int WPE>
 static void launch_trace(artes_grid* g, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
-    const size_t lds = LDS ? face_table_bytes(G.nr, G.ntheta, G.nphi) : 0;
+    const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
     int per_cu = 0;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, OBL, WPE, LDS>, BLOCK, lds);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, OBL, WPE>, BLOCK, lds);
     const char* bp = getenv("ARTES_TRACE_BPC");   // blocks per CU override (tuning)
     if (bp) per_cu = atoi(bp);
     g->trace_blocks = std::max(1, per_cu) * g->num_cus;
     timed(g, ARTES_K_TRACE, stream, [&] {
-        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, LDS>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
 }
 
-template <bool G3D, bool OBL>
-static void launch_trace_lds(artes_grid* g, int wpe, bool lds, const DevGrid& G, const DevRun& R, const Lists& L,
-                             hipStream_t stream) {
-    if (lds) {
-        if (wpe == 5) launch_trace<G3D, OBL, 5, true>(g, G, R, L, stream);
-        else launch_trace<G3D, OBL, 4, true>(g, G, R, L, stream);
-    } else {
-        if (wpe == 5) launch_trace<G3D, OBL, 5, false>(g, G, R, L, stream);
-        else launch_trace<G3D, OBL, 4, false>(g, G, R, L, stream);
-    }
-}
-
 // k_trace variant: 3D or radial-only grid, spheroidal (oblate) or spherical planet,
-// occupancy target and face tables in LDS or global memory
+// occupancy target (waves per SIMD the register budget is sized for)
 template <bool G3D>
-static void launch_trace_any(artes_grid* g, int wpe, bool lds, const DevGrid& G, const DevRun& R, const Lists& L,
-                             hipStream_t stream) {
+static void launch_trace_any(artes_grid* g, int wpe, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
     const bool oblate = !(G.ax2 == 1.0 && G.by2 == 1.0 && G.cz2 == 1.0 && G.a == 1.0 && G.b == 1.0);
-    if (oblate) launch_trace_lds<G3D, true>(g, wpe, lds, G, R, L, stream);
-    else launch_trace_lds<G3D, false>(g, wpe, lds, G, R, L, stream);
+    if (oblate) {
+        if (wpe == 3) launch_trace<G3D, true, 3>(g, G, R, L, stream);
+        else launch_trace<G3D, true, 4>(g, G, R, L, stream);
+    } else {
+        if (wpe == 3) launch_trace<G3D, false, 3>(g, G, R, L, stream);
+        else launch_trace<G3D, false, 4>(g, G, R, L, stream);
+    }
 }
 
 template <bool G3D>
@@ -298,10 +292,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     int* cnt = g->d_counts;
     const int side_blocks = std::max(1, g->num_cus * 8);
     const char* we = getenv("ARTES_WPE");
-    const int wpe = we ? atoi(we) : 5;
-    // face tables go to LDS unless they would cut the trace kernel's occupancy
-    const char* le = getenv("ARTES_LDS");
-    const bool use_lds = (le ? atoi(le) != 0 : true) && face_table_bytes(G.nr, G.ntheta, G.nphi) <= 32768;
+    const int wpe = we ? atoi(we) : 4;
+    if (trace_table_bytes(G.nr, G.ntheta, G.nphi) > 65536) return fail(-22, "face tables exceed the 64 KiB LDS budget of k_trace");
     auto lists = [&](int in) {
         Lists L;
         L.trace_in = g->d_lists[in]; L.trace_in_n = cnt + in;
@@ -332,7 +324,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const long long max_it = 2000000LL;
     for (;;) {
         Lists L = lists(in);
-        launch_trace_any<G3D>(g, wpe, use_lds, G, R, L, stream);
+        launch_trace_any<G3D>(g, wpe, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
             hipLaunchKernelGGL(k_event, dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
         });

@@ -1,4 +1,5 @@
-"""Lane occupancy of k_trace (needs the -DARTES_DEBUG_LANES build via ARTES_LIB_PATH)."""
+"""Lane occupancy of k_trace (needs the -DARTES_DEBUG_LANES build via ARTES_LIB_PATH).
+usage: python tools/lane_stats.py [packets] [ENV=VAL,ENV=VAL ...]  (one variant per argument)"""
 import os
 import sys
 
@@ -6,18 +7,32 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from artes_amd import driver, synthetic  # noqa: E402
 from artes_amd.engine import Grid  # noqa: E402
 
+n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 5 * 10**7
+variants = [dict(kv.split("=", 1) for kv in v.split(",")) if v else {} for v in (sys.argv[2:] or [""])]
 cfg = driver.default_config()
-for name in ("ray3d", "hg"):
+for name in ("ray3d",):
     atm = synthetic.make_config(name, share_matrix=True)
     det = driver.detector_geometry(cfg, atm["radial"][-1])
     g = Grid(atm, 0)
+    g.set_profiling(True)
     p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0))
-    for refill in ("16", "32", "48"):
-        os.environ["ARTES_REFILL"] = refill
-        n = 5 * 10**7
+    for env in variants:
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        g.run(p, 0, 10**5, 1)
+        g.kernel_times()
         r = g.run(p, 0, n, 2024)
+        kt = g.kernel_times()
         steps, lanes, refills = int(r.err[60]), int(r.err[61]), int(r.err[59])
+        tsteps, tlanes = int(r.err[54]), int(r.err[55])
         C = r.counter("crossings")
-        print(f"{name} refill {refill}: {g.last_kernel_ms():.1f} ms, wave-steps {steps:.3e}, lanes/step {lanes / steps:.1f}, "
-              f"crossings/wave-step {C / steps:.1f}, refills {refills:.3e} ({steps / refills:.1f} steps/refill)", flush=True)
+        print(f"{name} {env}: {g.last_kernel_ms():.1f} ms ({n / g.last_kernel_ms() / 1e3:.1f} Mpkt/s) trace {kt['trace'][0]:.1f} ms, "
+              f"wave-steps {steps:.3e}, lanes/step {lanes / steps:.1f}, crossings/wave-step {C / steps:.1f}, "
+              f"steps/refill {steps / max(refills, 1):.1f}, tail steps {tsteps / steps:.3f} at {tlanes / max(tsteps, 1):.1f} lanes",
+              flush=True)
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     g.close()
