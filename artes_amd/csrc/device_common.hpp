@@ -19,7 +19,7 @@ constexpr double TWO_PI = 2.0 * PI;
 
 // -------------------------------------------------------------- device data ---
 struct DevGrid {
-    int nr, ntheta, nphi, ncell;
+    int nr, ntheta, nphi, ncell, nmat;
     int cell_depth;
     double ax2, by2, cz2, a, b;
     double rtop;
@@ -119,15 +119,16 @@ __device__ __forceinline__ void quad_roots(double a, double b, double c, double&
     s0 = (ok && fabs(a) > 1.e-100) ? r0 : 0.0;
     s1 = (ok && fabs(q) > 1.e-100) ? r1 : 0.0;
 }
-// root selection block of cell_face (e.g. ARTES.f90:2897-2907)
+// root selection block of cell_face (e.g. ARTES.f90:2897-2907): the smaller root above
+// `tol`, 0 if none, if both are equal or if the choice is >= 1e100.  Written as selects:
+// the nested ifs of the reference compile to exec-mask branches on a wave.
 __device__ __forceinline__ double pick_root(double s0, double s1, double tol) {
-    if (s0 > tol && s1 <= tol && s0 < 1.e100) return s0;
-    if (s1 > tol && s0 <= tol && s1 < 1.e100) return s1;
-    if (s0 > tol && s1 > tol) {
-        if (s0 < 1.e100 && s0 < s1) return s0;
-        if (s1 < 1.e100 && s1 < s0) return s1;
-    }
-    return 0.0;
+    const bool p0 = s0 > tol, p1 = s1 > tol;
+    const double both = (s0 < s1) ? s0 : ((s1 < s0) ? s1 : 0.0);
+    double r = (p0 & p1) ? both : 0.0;
+    r = (p0 & !p1) ? s0 : r;
+    r = (!p0 & p1) ? s1 : r;
+    return (r < 1.e100) ? r : 0.0;
 }
 
 // theta cone x^2+y^2 = z^2 tan^2(theta_f) with the nappe filter (ARTES.f90:3026-3064)

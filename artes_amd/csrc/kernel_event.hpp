@@ -317,8 +317,32 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
     }
 }
 
-// peel-off contribution + scattering (ARTES.f90:4765-4984, 819-846)
-__global__ __launch_bounds__(BLOCK) void k_event(DevGrid G, DevRun R, Pool S, Lists L) {
+// doubles of LDS holding the scattering tables of k_event: matrices, cumulative
+// sampling tables and the azimuth tables
+__host__ __device__ inline size_t event_table_doubles(int nmat) {
+    return (size_t)nmat * (MAT_DOUBLES + CUM_DOUBLES) + 2 * (NANG + 1);
+}
+
+// peel-off contribution + scattering (ARTES.f90:4765-4984, 819-846).  With LDS_T the
+// scattering tables (one 31 KB set per distinct matrix) are staged in LDS: the angle
+// sampling is two binary searches whose every probe depends on the previous one, so each
+// probe's latency (LDS ~100 cycles, L2 ~500) is paid in full.
+template <bool LDS_T>
+__global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, Lists L) {
+    extern __shared__ double s_ev[];
+    DevGrid G = G0;
+    if constexpr (LDS_T) {
+        const int nm = G0.nmat * MAT_DOUBLES, nc = G0.nmat * CUM_DOUBLES;
+        double* m = s_ev;
+        double* c = m + nm;
+        double* a = c + nc;
+        double* b = a + (NANG + 1);
+        for (int i = threadIdx.x; i < nm; i += BLOCK) m[i] = G0.mats[i];
+        for (int i = threadIdx.x; i < nc; i += BLOCK) c[i] = G0.cums[i];
+        for (int i = threadIdx.x; i <= NANG; i += BLOCK) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
+        __syncthreads();
+        G.mats = m; G.cums = c; G.sc2 = a; G.ss2 = b;
+    }
     const int n = *L.event_n;
     const size_t plane = (size_t)R.nx * R.ny;
     double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;

@@ -135,20 +135,23 @@ __device__ __forceinline__ void family_candidates(const DevGrid& G, const TraceT
     const double rb0 = fast_div(qc0, q0);
     const double ra1 = fast_div(isP ? num1 : q1, isP ? den1 : qa1);
     const double rb1 = fast_div(qc1, q1);
-    if (isP) {
-        const bool on_p = (ft == 3);
-        const double sp0 = (!(on_p && fi == cp) && fabs(den0) > 0.0) ? ra0 : 0.0;
-        d_in = (sp0 > 1.e-15 && sp0 < 1.e100) ? sp0 : 0.0;
-        const bool ok1 = !(on_p && fi == pout) && fabs(den1) > 0.0;
-        d_out = (ok1 && ra1 > 1.e-15 && sp0 < 1.e100) ? ra1 : 0.0;   // sic: sp0 (ARTES.f90:3318, 3346)
-        return;
-    }
+    // phi rules (ARTES.f90:3311-3346)
+    const bool on_p = (ft == 3);
+    const double sp0 = (!(on_p && fi == cp) && fabs(den0) > 0.0) ? ra0 : 0.0;
+    const double p_in = (sp0 > 1.e-15 && sp0 < 1.e100) ? sp0 : 0.0;
+    const bool okp = !(on_p && fi == pout) && fabs(den1) > 0.0;
+    const double p_out = (okp && ra1 > 1.e-15 && sp0 < 1.e100) ? ra1 : 0.0;   // sic: sp0 (ARTES.f90:3318, 3346)
+    // quadratic roots; 0 where absent (ARTES.f90:4154-4173)
     const bool ok0 = disc0 >= 0.0, ok1 = disc1 >= 0.0;
     double s00 = (ok0 && fabs(qa0) > 1.e-100) ? ra0 : 0.0, s01 = (ok0 && fabs(q0) > 1.e-100) ? rb0 : 0.0;
     double s10 = (ok1 && fabs(qa1) > 1.e-100) ? ra1 : 0.0, s11 = (ok1 && fabs(q1) > 1.e-100) ? rb1 : 0.0;
     const int kout = kin + 1;
-    const int fl0 = isT ? T.tfl[kin] : 0, fl1 = isT ? T.tfl[kout] : 0;
-    if (isT) {   // nappe filter (ARTES.f90:3040-3064)
+    const int fl0 = T.tfl[isT ? kin : 0], fl1 = T.tfl[isT ? kout : 0];
+    // cone nappe filter (ARTES.f90:3040-3064): a root on the other nappe is no crossing
+    const bool g0 = isT && (fl0 & TF_GT90), l0 = isT && (fl0 & TF_LT90);
+    const bool g1 = isT && (fl1 & TF_GT90), l1 = isT && (fl1 & TF_LT90);
+    const double z00 = z + s00 * n2, z01 = z + s01 * n2, z10 = z + s10 * n2, z11 = z + s11 * n2;
+    if (isT) {
         auto wrong = [&](double s, int fl) {
             const double zz = z + s * n2;
             return s > 1.e-15 && ((zz > 0.0 && (fl & TF_GT90)) || (zz < 0.0 && (fl & TF_LT90)));
@@ -162,18 +165,15 @@ __device__ __forceinline__ void family_candidates(const DevGrid& G, const TraceT
     const bool same0 = (ft == ftype && fi == kin), same1 = (ft == ftype && fi == kout);
     const double p0 = pick_root(s00, s01, (same0 && isT) ? 1.e-3 : 1.e-15);
     const double p1 = pick_root(s10, s11, same1 ? 1.e-3 : 1.e-15);
-    if (isR) {
-        d_in = same0 ? 0.0 : p0;
-        d_out = p1;
-    } else {
-        double a, b;
-        if (fl0 & TF_CONE) a = (!same0 || (fl0 & TF_GT90)) ? p0 : 0.0;
-        else a = (!same0 && zp > 0.0 && n2 > 1.e-15) ? zp : 0.0;
-        if (fl1 & TF_CONE) b = (!same1 || (fl1 & TF_LT90)) ? p1 : 0.0;
-        else b = (!same1 && zp > 0.0 && n2 < -1.e-15) ? zp : 0.0;
-        d_in = (ct != 0) ? a : 0.0;
-        d_out = (kout != G.ntheta) ? b : 0.0;
-    }
+    // sphere rules: the inner sphere the packet sits on is no candidate
+    const double r_in = same0 ? 0.0 : p0, r_out = p1;
+    // theta rules: cone with the same-face filter, or the 90-degree plane (ARTES.f90:3066-3290)
+    const bool cone0 = fl0 & TF_CONE, cone1 = fl1 & TF_CONE;
+    const double ta = cone0 ? ((!same0 || (fl0 & TF_GT90)) ? p0 : 0.0) : ((!same0 && zp > 0.0 && n2 > 1.e-15) ? zp : 0.0);
+    const double tb = cone1 ? ((!same1 || (fl1 & TF_LT90)) ? p1 : 0.0) : ((!same1 && zp > 0.0 && n2 < -1.e-15) ? zp : 0.0);
+    const double t_in = (ct != 0) ? ta : 0.0, t_out = (kout != G.ntheta) ? tb : 0.0;
+    d_in = isP ? p_in : (isT ? t_in : r_in);
+    d_out = isP ? p_out : (isT ? t_out : r_out);
 }
 
 // -------------------------------------------------------------- k_trace ---

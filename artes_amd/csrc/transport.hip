@@ -294,6 +294,11 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const char* we = getenv("ARTES_WPE");
     const int wpe = we ? atoi(we) : 4;
     if (trace_table_bytes(G.nr, G.ntheta, G.nphi) > 65536) return fail(-22, "face tables exceed the 64 KiB LDS budget of k_trace");
+    // scattering tables in LDS for k_event when they fit next to one another (a few
+    // distinct matrices: uniform and layered atmospheres); otherwise read from L2
+    const size_t ev_bytes = event_table_doubles(G.nmat) * sizeof(double);
+    const char* el = getenv("ARTES_EVENT_LDS");
+    const bool ev_lds = (el ? atoi(el) != 0 : true) && ev_bytes <= 65536;
     auto lists = [&](int in) {
         Lists L;
         L.trace_in = g->d_lists[in]; L.trace_in_n = cnt + in;
@@ -326,7 +331,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         Lists L = lists(in);
         launch_trace_any<G3D>(g, wpe, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
-            hipLaunchKernelGGL(k_event, dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+            if (ev_lds) hipLaunchKernelGGL(k_event<true>, dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
+            else hipLaunchKernelGGL(k_event<false>, dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
         });
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
@@ -371,7 +377,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     HIP_TRY(hipMemsetAsync(g->d_copies, 0, stride * NCOPY * sizeof(double), stream));
 
     DevGrid G;
-    G.nr = T.nr; G.ntheta = T.ntheta; G.nphi = T.nphi; G.ncell = T.ncell;
+    G.nr = T.nr; G.ntheta = T.ntheta; G.nphi = T.nphi; G.ncell = T.ncell; G.nmat = T.nmat;
     G.cell_depth = p->cell_depth >= 0 ? p->cell_depth : T.cell_depth[p->wl_index];
     G.ax2 = 1.0 / (T.oblate_x * T.oblate_x); G.by2 = 1.0 / (T.oblate_y * T.oblate_y); G.cz2 = 1.0 / (T.oblate_z * T.oblate_z);
     G.a = 1.0 / T.oblate_x; G.b = 1.0 / T.oblate_y;
