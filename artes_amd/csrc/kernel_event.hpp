@@ -194,8 +194,10 @@ __device__ __forceinline__ void start_prop(const Pool& S, int slot, double tau) 
 }
 
 // one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended)
+// `acc` takes moments 0-8 (I Q U V sums, their squares, the count) at plane stride `plane`:
+// the block's LDS detector or the global copy; `det` (global) takes moments 12-15
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
-                                         size_t plane, uint32_t& c_scat, uint32_t& c_det) {
+                                         double* __restrict__ acc, size_t plane, uint32_t& c_scat, uint32_t& c_det) {
     {
         const int m = S.s[slot].mode;
         if (m & FLAG_ERR) { S.s[slot].mode = S_END_DROP; return 2; }
@@ -272,11 +274,11 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                         }
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
-                            unsafeAtomicAdd(&det[q * plane + pix], v[q]);
-                            unsafeAtomicAdd(&det[(4 + q) * plane + pix], v[q] * v[q]);
+                            unsafeAtomicAdd(&acc[q * plane + pix], v[q]);
+                            unsafeAtomicAdd(&acc[(4 + q) * plane + pix], v[q] * v[q]);
                             cs[q] += v[q];
                         }
-                        unsafeAtomicAdd(&det[8 * plane + pix], 1.0);
+                        unsafeAtomicAdd(&acc[8 * plane + pix], 1.0);
                         S.s[slot].cs0 = cs[0]; S.s[slot].cs1 = cs[1]; S.s[slot].cs2 = cs[2]; S.s[slot].cs3 = cs[3];
                         S.s[slot].pt0 += v[0]; S.s[slot].pt1 += v[1]; S.s[slot].pt2 += v[2]; S.s[slot].pt3 += v[3];
                         S.s[slot].peel_sum += wI;
@@ -323,14 +325,20 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
     return (size_t)nmat * (MAT_DOUBLES + CUM_DOUBLES) + 2 * (NANG + 1);
 }
 
-// peel-off contribution + scattering (ARTES.f90:4765-4984, 819-846).  With LDS_T the
-// scattering tables (one 31 KB set per distinct matrix) are staged in LDS: the angle
-// sampling is two binary searches whose every probe depends on the previous one, so each
-// probe's latency (LDS ~100 cycles, L2 ~500) is paid in full.
-template <bool LDS_T>
+// peel-off contribution + scattering (ARTES.f90:4765-4984, 819-846).
+//  LDS_T: the scattering tables (one 31 KB set per distinct matrix) are staged in LDS --
+//         the angle sampling is two binary searches whose every probe depends on the
+//         previous one, so each probe's latency (LDS ~100 cycles, L2 ~500) is paid in full.
+//  LDS_D: the block accumulates moments 0-8 of the detector in LDS and adds them to its
+//         HBM copy once at the end.  Float atomics to HBM execute at the memory side and
+//         stay in vmcnt for thousands of cycles, so every later load of the wave waited
+//         for them; the grid is one wave of resident blocks, each looping over many events.
+template <bool LDS_T, bool LDS_D>
 __global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, Lists L) {
     extern __shared__ double s_ev[];
     DevGrid G = G0;
+    const size_t plane = (size_t)R.nx * R.ny;
+    double* lds_next = s_ev;
     if constexpr (LDS_T) {
         const int nm = G0.nmat * MAT_DOUBLES, nc = G0.nmat * CUM_DOUBLES;
         double* m = s_ev;
@@ -340,19 +348,31 @@ __global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, L
         for (int i = threadIdx.x; i < nm; i += BLOCK) m[i] = G0.mats[i];
         for (int i = threadIdx.x; i < nc; i += BLOCK) c[i] = G0.cums[i];
         for (int i = threadIdx.x; i <= NANG; i += BLOCK) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
-        __syncthreads();
         G.mats = m; G.cums = c; G.sc2 = a; G.ss2 = b;
+        lds_next = b + (NANG + 1);
     }
-    const int n = *L.event_n;
-    const size_t plane = (size_t)R.nx * R.ny;
     double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
+    double* __restrict__ acc = det;
+    if constexpr (LDS_D) {
+        acc = lds_next;
+        for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) acc[i] = 0.0;
+    }
+    if constexpr (LDS_T || LDS_D) __syncthreads();
+    const int n = *L.event_n;
     uint32_t c_scat = 0, c_det = 0;
     const int n_pad = (n + 63) & ~63;   // whole waves iterate together (wave-aggregated appends)
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
         const int slot = i < n ? L.event[i] : -1;
-        const int dest = slot >= 0 ? event_one(G, R, S, slot, det, plane, c_scat, c_det) : 0;
+        const int dest = slot >= 0 ? event_one(G, R, S, slot, det, acc, plane, c_scat, c_det) : 0;
         wave_append(dest == 1, slot, L.trace_out, L.trace_out_n);
         wave_append(dest == 2, slot, L.emit, L.emit_n);
+    }
+    if constexpr (LDS_D) {
+        __syncthreads();
+        for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) {
+            const double v = acc[i];
+            if (v != 0.0) unsafeAtomicAdd(&det[i], v);
+        }
     }
     const unsigned long long ws = wave_sum_u64(c_scat), wd = wave_sum_u64(c_det);
     if ((threadIdx.x & 63) == 0) {

@@ -299,6 +299,20 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const size_t ev_bytes = event_table_doubles(G.nmat) * sizeof(double);
     const char* el = getenv("ARTES_EVENT_LDS");
     const bool ev_lds = (el ? atoi(el) != 0 : true) && ev_bytes <= 65536;
+    // detector moments 0-8 accumulated per k_event block in LDS when they fit
+    const size_t det_bytes = 9 * (size_t)R.nx * R.ny * sizeof(double);
+    const char* dl = getenv("ARTES_DET_LDS");
+    const bool det_lds = (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
+    int ev_blocks = side_blocks;
+    if (det_lds) {
+        int per_cu = 0;
+        const size_t b = (ev_lds ? ev_bytes : 0) + det_bytes;
+        if (ev_lds) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_event<true, true>, BLOCK, b);
+        else hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_event<false, true>, BLOCK, b);
+        const char* eb = getenv("ARTES_EVENT_BPC");
+        if (eb) per_cu = atoi(eb);
+        ev_blocks = std::max(1, per_cu) * g->num_cus;
+    }
     auto lists = [&](int in) {
         Lists L;
         L.trace_in = g->d_lists[in]; L.trace_in_n = cnt + in;
@@ -331,8 +345,10 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         Lists L = lists(in);
         launch_trace_any<G3D>(g, wpe, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
-            if (ev_lds) hipLaunchKernelGGL(k_event<true>, dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
-            else hipLaunchKernelGGL(k_event<false>, dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+            if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
+            else if (ev_lds) hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
+            else if (det_lds) hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L);
+            else hipLaunchKernelGGL((k_event<false, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
         });
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
