@@ -90,26 +90,32 @@ __device__ __forceinline__ void unpack_cell(int c, int& r, int& t, int& p) { r =
 __device__ __forceinline__ int pack_face(int type, int idx) { return (type << 28) | (idx & 0x0FFFFFFF); }
 __device__ __forceinline__ void unpack_face(int f, int& type, int& idx) { type = (f >> 28) & 0xF; idx = f & 0x0FFFFFFF; if (idx == 0x0FFFFFFF) idx = -1; }
 
-// Work distribution over the trace list: the first `n_static` entries are split into one
-// contiguous chunk per wave (no atomics: a wave-local cursor), the rest is grabbed
-// dynamically through 8 sharded cursors to balance the tail.  Device-scope atomics are
-// resolved at the memory side (~µs round trip), so a purely dynamic grab stalls every
-// refill; the static part keeps most refills at one list load + one record load.
+// Work distribution over the trace list: the first `n_static` entries are split into
+// 64-entry chunks dealt round-robin to the waves (chunk w, w+W, w+2W, ... for wave w; no
+// atomics, a wave-local cursor), the rest is grabbed dynamically through 8 sharded
+// cursors to balance the tail.  Device-scope atomics are resolved at the memory side
+// (~µs round trip), so a purely dynamic grab stalls every refill.  The list arrives in
+// the order packets finished their previous trace, which correlates with how long their
+// next trace runs; dealing chunks round-robin gives every wave a sample of the whole list.
 struct TraceCursor {
-    int pos, end;              // static chunk of this wave (wave-uniform)
+    int pos, end;              // current static chunk of this wave (wave-uniform)
+    int chunk, nchunk, stride; // chunk index, static chunk count, waves in the grid
     int dyn_lo, dyn_n;         // dynamic range
     bool exhausted;
 };
 
 __device__ __forceinline__ TraceCursor make_cursor(int n, int static_q64) {
-    const long long W = (long long)gridDim.x * (BLOCK / 64);
-    const long long w = (long long)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
-    const int n_static = (int)(((long long)n * static_q64) >> 6);
+    const int W = (int)gridDim.x * (BLOCK / 64);
+    const int w = (int)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+    const int nchunk = (int)((((long long)n * static_q64) >> 6) >> 6);
     TraceCursor c;
-    c.pos = (int)((n_static * w) / W);
-    c.end = (int)((n_static * (w + 1)) / W);
-    c.dyn_lo = n_static;
-    c.dyn_n = n - n_static;
+    c.chunk = w;
+    c.nchunk = nchunk;
+    c.stride = W;
+    c.pos = w * 64;
+    c.end = (w < nchunk) ? c.pos + 64 : c.pos;
+    c.dyn_lo = nchunk * 64;
+    c.dyn_n = n - nchunk * 64;
     c.exhausted = (n == 0);
     return c;
 }
@@ -122,9 +128,17 @@ __device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, 
     const int rank = __popcll(mask & ((1ULL << lane) - 1ULL));
     int got = 0, mine = -1;
     if (c.pos < c.end) {
-        got = min(k, c.end - c.pos);
-        if (need && rank < got) mine = c.pos + rank;
-        c.pos += got;
+        for (int part = 0; part < 2 && got < k && c.pos < c.end; part++) {   // current chunk, then the next
+            const int take = min(k - got, c.end - c.pos);
+            if (need && rank >= got && rank < got + take) mine = c.pos + (rank - got);
+            got += take;
+            c.pos += take;
+            if (c.pos == c.end) {
+                c.chunk += c.stride;
+                c.pos = c.chunk * 64;
+                c.end = (c.chunk < c.nchunk) ? c.pos + 64 : c.pos;
+            }
+        }
         return mine;
     }
     for (int a = 0; a < 8 && got < k; a++) {
@@ -364,7 +378,9 @@ __global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, L
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
         const int slot = i < n ? L.event[i] : -1;
         const int dest = slot >= 0 ? event_one(G, R, S, slot, det, acc, plane, c_scat, c_det) : 0;
-        wave_append(dest == 1, slot, L.trace_out, L.trace_out_n);
+        // the next propagation trace goes to the same position of the output trace list
+        // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
+        if (i < n) L.trace_out[i] = (dest == 1) ? slot : -1;
         wave_append(dest == 2, slot, L.emit, L.emit_n);
     }
     if constexpr (LDS_D) {
@@ -382,9 +398,16 @@ __global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, L
 }
 
 // close finished packets and emit new ones (ARTES.f90:546-597, 1027-1115, 2605-2669)
+//
+// Emit-list entry i takes packet id next_pkt + i (ids < n only) and writes its new trace
+// to position event_n + i of the output trace list (k_event filled [0, event_n)), a hole
+// (-1) when the ids have run out: list positions and packet ids need no atomics, and the
+// packet-to-slot assignment is deterministic.  k_rotate advances next_pkt and the count.
 template <bool G3D, bool TRACE>
 __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lists L) {
     const int n = *L.emit_n;
+    const int out0 = *L.event_n;
+    const unsigned long long pkt0 = *L.next_pkt;
     const size_t plane = (size_t)R.nx * R.ny;
     double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
     uint32_t c_exit = 0, c_abs = 0, c_drop = 0, c_pkt = 0;
@@ -415,19 +438,9 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
                 rr[3] = (double)(m - S_END_EXIT + 1);   // 1 exit, 2 absorbed, 3 dropped
             }
         }
-        // packet ids for the lanes that need one: one atomic per wave
-        const bool need = (m != S_RETIRED);
-        const unsigned long long mask = __ballot(need);
-        unsigned long long k = 0;
-        if (mask) {
-            const int leader = __ffsll((long long)mask) - 1;
-            unsigned long long base = 0;
-            if (lane == leader) base = atomicAdd(L.next_pkt, (unsigned long long)__popcll(mask));
-            base = __shfl(base, leader);
-            k = base + __popcll(mask & ((1ULL << lane) - 1ULL));
-        }
-        const bool emit = need && k < R.n;
-        if (need && !emit) S.s[slot].mode = S_RETIRED;
+        const unsigned long long k = pkt0 + (unsigned long long)i;
+        const bool emit = slot >= 0 && k < R.n;
+        if (slot >= 0 && !emit) S.s[slot].mode = S_RETIRED;
         if (emit) {
         c_pkt++;
         const unsigned long long pid = R.first + k;
@@ -489,7 +502,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         S.s[slot].ncross = 0;
         S.s[slot].mode = S_FIRST;
         }   // emit
-        wave_append(emit, slot, L.trace_out, L.trace_out_n);
+        if (i < n) L.trace_out[out0 + i] = emit ? slot : -1;
     }
     const unsigned long long a = wave_sum_u64(c_exit), b = wave_sum_u64(c_abs), c = wave_sum_u64(c_drop),
                              d = wave_sum_u64(c_pkt);
@@ -516,12 +529,16 @@ __global__ void k_init(Pool S, int* emit, int* emit_n) {
     if (i == 0) *emit_n = S.P;
 }
 
-// end of an iteration: the output trace list becomes the input, the consumed input
-// buffer is reset to become the next output; event/emit lists and cursors are zeroed
-__global__ void k_rotate(int* in_n, int* out_n, int* event_n, int* emit_n, unsigned int* grab) {
+// end of an iteration: the output trace list (k_event's event_n entries, then k_emit's
+// emit_n) becomes the input, the consumed input buffer is reset to become the next
+// output, packet ids advance by the emit-list length; event/emit lists and cursors are zeroed
+__global__ void k_rotate(int* in_n, int* out_n, int* event_n, int* emit_n, unsigned int* grab,
+                         unsigned long long* next_pkt) {
     if (threadIdx.x == 0) {
-        *in_n = 0;          // this buffer is the next iteration's output
-        (void)out_n;        // keeps its count: it is the next iteration's input
+        const int ev = *event_n, em = *emit_n;
+        *out_n = ev + em;
+        *next_pkt += (unsigned long long)em;
+        *in_n = 0;
         *event_n = 0;
         *emit_n = 0;
     }

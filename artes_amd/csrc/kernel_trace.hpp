@@ -230,8 +230,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
                 dbg_refills++;
 #endif
-                if (!have && my >= 0) {
-                    slot = L.trace_in[my];
+                if (!have && my >= 0) slot = L.trace_in[my];
+                if (!have && my >= 0 && slot >= 0) {   // -1: a hole left by a dropped or retired packet
                     const Slot* rec = S.s + slot;
                     mode = rec->mode;
                     px = rec->px; py = rec->py; pz = rec->pz;
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }
         }
-        if (!__any(have)) break;
+        if (!__any(have) && cur.exhausted) break;   // (all lanes idle otherwise: every grab was a hole)
 #ifdef ARTES_DEBUG_LANES
         dbg_steps++;
         dbg_lanes += __popcll(__ballot(have));

@@ -334,7 +334,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         Lists L = lists(1);   // trace_out = list 0
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
-            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + 1, cnt + 0, cnt + 2, cnt + 3, g->d_grab);
+            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + 1, cnt + 0, cnt + 2, cnt + 3, g->d_grab, g->d_next);
         });
     }
     HIP_TRY(hipGetLastError());
@@ -352,7 +352,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         });
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
-            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + in, cnt + (1 - in), cnt + 2, cnt + 3, g->d_grab);
+            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + in, cnt + (1 - in), cnt + 2, cnt + 3, g->d_grab, g->d_next);
         });
         in = 1 - in;
         it++;
