@@ -37,16 +37,26 @@ struct DevGrid {
     const double* __restrict__ cums;     // [nmat][181][4]
     const double* __restrict__ sc2;      // [181]
     const double* __restrict__ ss2;      // [181]
+    // thermal source and surface (photon:source=planet, planet:surface_albedo)
+    const double* __restrict__ rfr;      // rfront [nr+1]
+    const double* __restrict__ tcos;     // cos(theta_f) [ntheta+1]
+    const double* __restrict__ th_cdf;   // emissivity CDF [(nr-cell_depth)*ntheta*nphi], order (i, j, k)
+    const double* __restrict__ th_weight;   // cell_weight [ncell]
+    int th_ncdf, th_cd0;                 // CDF length; radial index of its first entry
+    double th_total;
+    double ox, oy, oz;                   // oblate_x, oblate_y, oblate_z (ARTES.f90:469-471)
 };
 
 struct DevRun {
     uint64_t first, n, seed;
     int nx, ny, photon_scattering, phase_far, stellar_direction, defer, refill, static_q64;
+    int photon_source, photon_emission;
+    double photon_bias;
     double det0, det1, det2, sdt, cdt, sdp, cdp;
     double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
     double* __restrict__ det;       // [NCOPY][4][4][ny][nx]
     size_t det_stride;              // doubles per copy
-    double* __restrict__ tot2;      // [4] packet-level sum T^2 per Stokes
+    double* __restrict__ tot2;      // [6] packet-level sum T^2 per Stokes, flux_emitted, flux_exit
     unsigned long long* __restrict__ cnt;   // [ARTES_NUM_COUNTERS]
     unsigned long long* __restrict__ err;   // [ARTES_NUM_ERR]
     double* __restrict__ rec;       // [n][4] (TRACE builds)

@@ -47,7 +47,8 @@ struct alignas(256) Slot {
     int mode, ncross;
     double wI;                          // Stokes I including the weights applied in k_trace
     double tpeel;                       // optical depth of the last peel-off trace
-    double spare0[3];
+    double cos_surf;                    // surface peel: cos(normal, detector) (ARTES.f90:4623)
+    double spare0[2];
     // line 1: event state
     double s0, s1, s2, s3;              // Stokes vector as of the last scattering
     double cs0, cs1, cs2, cs3;          // running contribution to the current pixel
@@ -78,12 +79,22 @@ struct Lists {
 enum SlotMode : int {
     S_FRESH = 0,        // never held a packet
     S_FIRST = 1, S_PROP = 2, S_PEEL = 3,       // trace kinds (in a trace list)
-    S_PEEL_DONE = 4,    // in the event list; bit 8 = exit, bit 9 = cell error
+    S_PEEL_DONE = 4,    // in the event list; bit 8 = exit, bit 9 = cell error, bits 10-11 = peel kind
     S_END_EXIT = 5, S_END_ABS = 6, S_END_DROP = 7,   // in the emit list
     S_RETIRED = 8,
+    S_PEEL_T = 9,       // trace: thermal emission peel-off (peel_thermal, ARTES.f90:4519-4598)
+    S_PEEL_S = 10,      // trace: surface peel-off (peel_surface, ARTES.f90:4600-4708)
+    S_SURF_HIT = 11,    // in the event list: Lambertian reflection pending (ARTES.f90:764-772)
 };
 constexpr int FLAG_EXIT = 1 << 8;
 constexpr int FLAG_ERR = 1 << 9;
+constexpr int PEEL_KIND_SHIFT = 10;   // 0 = after scattering, 1 = thermal, 2 = surface
+
+__device__ __forceinline__ bool is_peel_trace(int mode) { return mode == S_PEEL || mode == S_PEEL_T || mode == S_PEEL_S; }
+__device__ __forceinline__ bool to_event_list(int end) {
+    const int b = end & 0xFF;
+    return b == S_PEEL_DONE || b == S_SURF_HIT;
+}
 
 __device__ __forceinline__ int pack_cell(int r, int t, int p) { return r | (t << 12) | (p << 22); }
 __device__ __forceinline__ void unpack_cell(int c, int& r, int& t, int& p) { r = c & 0xFFF; t = (c >> 12) & 0x3FF; p = (c >> 22) & 0x3FF; }
@@ -207,13 +218,110 @@ __device__ __forceinline__ void start_prop(const Pool& S, int slot, double tau) 
     S.s[slot].mode = S_PROP;
 }
 
+// detector pixel of a peel from (px, py, pz) (ARTES.f90:4947-4951); -1 outside the image
+__device__ __forceinline__ int peel_pixel(const DevRun& R, double px, double py, double pz) {
+    const double x_im = py * R.cdp - px * R.sdp;
+    const double y_im = pz * R.sdt - py * R.cdt * R.sdp - px * R.cdt * R.cdp;
+    const int ix = (int)((double)R.nx * (x_im + R.x_max) / (2.0 * R.x_max));
+    const int iy = (int)((double)R.ny * (y_im + R.y_max) / (2.0 * R.y_max));
+    if (ix < 0 || ix >= R.nx || iy < 0 || iy >= R.ny) return -1;
+    return iy * R.nx + ix;
+}
+
+// a peel that carries Stokes I only (peel_thermal 4577-4583, peel_surface 4684-4690):
+// moments 0 and 4, and the I-only count plane 9 (the reference counts it for I alone)
+__device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
+                                           double* __restrict__ acc, size_t plane, double v, int err_code,
+                                           uint32_t& c_det) {
+    if (!(v > 0.0 && v < 1.e100)) { log_err(R, err_code); return; }
+    const int pix = peel_pixel(R, S.s[slot].px, S.s[slot].py, S.s[slot].pz);
+    if (pix < 0) { log_err(R, 63); return; }
+    unsafeAtomicAdd(&acc[0 * plane + pix], v);
+    unsafeAtomicAdd(&acc[4 * plane + pix], v * v);
+    unsafeAtomicAdd(&acc[9 * plane + pix], 1.0);
+    const int cur = S.s[slot].cur_pix;
+    double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
+    if (pix != cur) {
+        if (cur >= 0) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
+        }
+        S.s[slot].cur_pix = pix;
+        cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
+    }
+    S.s[slot].cs0 = cs[0] + v; S.s[slot].cs1 = cs[1]; S.s[slot].cs2 = cs[2]; S.s[slot].cs3 = cs[3];
+    S.s[slot].pt0 += v;
+    S.s[slot].peel_sum += v;
+    c_det++;
+}
+
+// outward unit normal of the (oblate) surface at (x, y, z) (ARTES.f90:1378-1384)
+__device__ __forceinline__ void surface_normal(const DevGrid& G, double x, double y, double z, double& n0, double& n1, double& n2) {
+    n0 = x / (G.ox * G.ox); n1 = y / (G.oy * G.oy); n2 = z / (G.oz * G.oz);
+    const double norm = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+    n0 /= norm; n1 /= norm; n2 /= norm;
+}
+
+// thermal-emission peel done (ARTES.f90:599-622, 4566-4591), then the first optical
+// depth trace of the packet; returns 1 (next trace) or 2 (dropped)
+__device__ __forceinline__ int event_thermal(const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
+                                             double* __restrict__ acc, size_t plane, uint32_t& c_det) {
+    const int m = S.s[slot].mode;
+    if (m & FLAG_ERR) { log_err(R, 47); S.s[slot].mode = S_END_DROP; return 2; }
+    const double tau = S.s[slot].tpeel;
+    if ((m & FLAG_EXIT) && tau < 50.0)
+        add_peel_I(R, S, slot, det, acc, plane, exp(-tau) / (4.0 * PI) * S.s[slot].wI, 51, c_det);
+    S.s[slot].mode = S_FIRST;
+    return 1;
+}
+
+// Lambertian reflection (ARTES.f90:1369-1402) at the surface point stored in the slot by
+// k_trace, then the surface peel trace if the detector sees the surface element
+// (4616-4631), else straight back to the interrupted propagation trace
+__device__ __forceinline__ int event_surface_hit(const DevGrid& G, const DevRun& R, const Pool& S, int slot) {
+    const double px = S.s[slot].px, py = S.s[slot].py, pz = S.s[slot].pz;
+    double n0, n1, n2;
+    surface_normal(G, px, py, pz, n0, n1, n2);
+    Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
+    const double alpha = sqrt(rng.uni());
+    const double beta = TWO_PI * rng.uni();
+    double e0, e1, e2;
+    direction_cosine(R, alpha, beta, n0, n1, n2, e0, e1, e2);
+    S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
+    S.s[slot].dx = e0; S.s[slot].dy = e1; S.s[slot].dz = e2;
+    // the surface depolarises (ARTES.f90:1396-1400); I carries k_trace's weights
+    const double wI = S.s[slot].wI;
+    S.s[slot].s0 = wI; S.s[slot].s1 = 0.0; S.s[slot].s2 = 0.0; S.s[slot].s3 = 0.0;
+    // cos of the angle between the surface normal and the detector (4623-4625)
+    const double cos_angle = n0 * R.det0 + n1 * R.det1 + n2 * R.det2;
+    S.s[slot].cos_surf = cos_angle;
+    S.s[slot].mode = cos_angle > 0.0 ? S_PEEL_S : S_PROP;
+    return 1;
+}
+
+// surface peel done (ARTES.f90:4633-4700), then the interrupted propagation resumes
+__device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
+                                                  double* __restrict__ acc, size_t plane, uint32_t& c_det) {
+    const int m = S.s[slot].mode;
+    const double tau = S.s[slot].tpeel;
+    if (!(m & FLAG_ERR) && (m & FLAG_EXIT) && tau < 50.0)
+        add_peel_I(R, S, slot, det, acc, plane, exp(-tau) * S.s[slot].cos_surf / PI * S.s[slot].wI, 52, c_det);
+    S.s[slot].mode = S_PROP;
+    return 1;
+}
+
 // one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended)
-// `acc` takes moments 0-8 (I Q U V sums, their squares, the count) at plane stride `plane`:
+// `acc` takes planes 0-9 (I Q U V sums, their squares, the peel count, the I-only count)
+// at plane stride `plane`:
 // the block's LDS detector or the global copy; `det` (global) takes moments 12-15
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
                                          double* __restrict__ acc, size_t plane, uint32_t& c_scat, uint32_t& c_det) {
     {
         const int m = S.s[slot].mode;
+        if ((m & 0xFF) == S_SURF_HIT) return event_surface_hit(G, R, S, slot);
+        const int kind = (m >> PEEL_KIND_SHIFT) & 3;
+        if (kind == 1) return event_thermal(R, S, slot, det, acc, plane, c_det);
+        if (kind == 2) return event_surface_peel(R, S, slot, det, acc, plane, c_det);
         if (m & FLAG_ERR) { S.s[slot].mode = S_END_DROP; return 2; }
         const double px = S.s[slot].px, py = S.s[slot].py, pz = S.s[slot].pz;
         double dx = S.s[slot].dx, dy = S.s[slot].dy, dz = S.s[slot].dz;
@@ -343,7 +451,7 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
 //  LDS_T: the scattering tables (one 31 KB set per distinct matrix) are staged in LDS --
 //         the angle sampling is two binary searches whose every probe depends on the
 //         previous one, so each probe's latency (LDS ~100 cycles, L2 ~500) is paid in full.
-//  LDS_D: the block accumulates moments 0-8 of the detector in LDS and adds them to its
+//  LDS_D: the block accumulates planes 0-9 of the detector in LDS and adds them to its
 //         HBM copy once at the end.  Float atomics to HBM execute at the memory side and
 //         stay in vmcnt for thousands of cycles, so every later load of the wave waited
 //         for them; the grid is one wave of resident blocks, each looping over many events.
@@ -369,7 +477,7 @@ __global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, L
     double* __restrict__ acc = det;
     if constexpr (LDS_D) {
         acc = lds_next;
-        for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) acc[i] = 0.0;
+        for (size_t i = threadIdx.x; i < 10 * plane; i += BLOCK) acc[i] = 0.0;
     }
     if constexpr (LDS_T || LDS_D) __syncthreads();
     const int n = *L.event_n;
@@ -385,7 +493,7 @@ __global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, L
     }
     if constexpr (LDS_D) {
         __syncthreads();
-        for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) {
+        for (size_t i = threadIdx.x; i < 10 * plane; i += BLOCK) {
             const double v = acc[i];
             if (v != 0.0) unsafeAtomicAdd(&det[i], v);
         }
@@ -395,6 +503,57 @@ __global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, L
         if (ws) atomicAdd(&R.cnt[ARTES_CNT_SCATTERS], ws);
         if (wd) atomicAdd(&R.cnt[ARTES_CNT_DETECTED], wd);
     }
+}
+
+// emit_photon, planet branch (ARTES.f90:1117-1266): a cell drawn from the emissivity CDF
+// (a binary search finds the entry the reference's linear scan stops at, 1126-1154), a
+// uniform point in it, and an isotropic or upward-biased direction
+__device__ __forceinline__ void emit_planet(const DevGrid& G, const DevRun& R, Rng& rng, double& px, double& py, double& pz,
+                                            double& dx, double& dy, double& dz, int& cr, int& ct, int& cp, double& bias) {
+    bias = 1.0;
+    const double samp = rng.uni() * G.th_total;
+    int lo = 0, hi = G.th_ncdf - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (G.th_cdf[mid] >= samp) hi = mid;
+        else lo = mid + 1;
+    }
+    const int per_r = G.ntheta * G.nphi;
+    cr = G.th_cd0 + lo / per_r; ct = (lo / G.nphi) % G.ntheta; cp = lo % G.nphi;
+    const double r = G.rfr[cr] + rng.uni() * (G.rfr[cr + 1] - G.rfr[cr]);
+    const double ctheta = G.tcos[ct] + rng.uni() * (G.tcos[ct + 1] - G.tcos[ct]);
+    const double stheta = sqrt(1.0 - ctheta * ctheta);
+    double ph;
+    const double xi = rng.uni();
+    if (G.nphi == 1) ph = TWO_PI * xi;
+    else if (cp < G.nphi - 1) ph = G.phif[cp] + xi * (G.phif[cp + 1] - G.phif[cp]);
+    else ph = G.phif[cp] + xi * (TWO_PI - G.phif[cp]);
+    const double cph = cos_b(ph);
+    double sph = sqrt(1.0 - cph * cph);
+    if (ph > PI) sph = -sph;
+    px = G.ox * (r * stheta * cph);
+    py = G.oy * (r * stheta * sph);
+    pz = G.oz * (r * ctheta);
+    if (R.photon_emission == 2) {   // biased upward (Gordon 1987), ARTES.f90:1233-1254
+        const double b = R.photon_bias;
+        const double yb = (1.0 + b) * tan(PI * rng.uni() / 2.0) / sqrt(1.0 - b * b);
+        const double ths = acos((1.0 - yb * yb) / (1.0 + yb * yb));
+        const double beta = TWO_PI * rng.uni();
+        double n0, n1, n2;
+        surface_normal(G, px, py, pz, n0, n1, n2);
+        direction_cosine(R, cos_b(PI - ths), beta, n0, n1, n2, dx, dy, dz);
+        bias = (PI * sin_b(ths) * (1.0 + b * cos_b(ths))) / (2.0 * sqrt(1.0 - b * b));
+    } else {                        // isotropic, ARTES.f90:1218-1231
+        const double alpha = 2.0 * rng.uni() - 1.0;
+        const double beta = TWO_PI * rng.uni();
+        const double cb = cos_b(beta);
+        double sb = sqrt(1.0 - cb * cb);
+        if (beta > PI) sb = -sb;
+        dx = sqrt(1.0 - alpha * alpha) * cb;
+        dy = sqrt(1.0 - alpha * alpha) * sb;
+        dz = alpha;
+    }
+    if (fabs(dz) >= 1.0) log_err(R, 54);
 }
 
 // close finished packets and emit new ones (ARTES.f90:546-597, 1027-1115, 2605-2669)
@@ -412,6 +571,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
     double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
     uint32_t c_exit = 0, c_abs = 0, c_drop = 0, c_pkt = 0;
     double t2[4] = {0, 0, 0, 0};
+    double f_emit = 0.0, f_exit = 0.0;   // thermal flux_emitted / flux_exit (ARTES.f90:607, 780, 953)
     const int n_pad = (n + 63) & ~63;
     const int lane = threadIdx.x & 63;
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
@@ -428,6 +588,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
                 unsafeAtomicAdd(&det[14 * plane + cur], S.s[slot].cs2 * S.s[slot].cs2);
                 unsafeAtomicAdd(&det[15 * plane + cur], S.s[slot].cs3 * S.s[slot].cs3);
             }
+            if (m == S_END_EXIT && R.photon_source == 2) f_exit += S.s[slot].wI;
             const double a0 = S.s[slot].pt0, a1 = S.s[slot].pt1, a2 = S.s[slot].pt2, a3 = S.s[slot].pt3;
             t2[0] += a0 * a0; t2[1] += a1 * a1; t2[2] += a2 * a2; t2[3] += a3 * a3;
             if constexpr (TRACE) {
@@ -446,6 +607,17 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         const unsigned long long pid = R.first + k;
         Rng rng;
         rng.seed(R.seed, pid);
+        double px, py, pz, dx, dy, dz, wI = 1.0;
+        int cr = G.nr - 1, ct = 0, cp = 0, face = pack_face(1, G.nr), mode0 = S_FIRST;
+        if (R.photon_source == 2) {
+            double bias;
+            emit_planet(G, R, rng, px, py, pz, dx, dy, dz, cr, ct, cp, bias);
+            // weight for the cell emission probability (ARTES.f90:605), then peel_thermal
+            wI = bias / G.th_weight[cr + G.nr * (ct + G.ntheta * cp)];
+            f_emit += wI;
+            face = pack_face(0, 0);
+            mode0 = S_PEEL_T;
+        } else {
         // emit_photon, star branch (ARTES.f90:1027-1115)
         const double Rt = G.rtop;
         double r_disk, phi_disk;
@@ -459,8 +631,8 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         double sphi, cphi;
         sincos_bounded(phi_disk, sphi, cphi);
         const double d1 = Rt * r_disk * sphi, d2 = Rt * r_disk * cphi;
-        double dx = -1.0, dy = 0.0, dz = 0.0;
-        double px = sqrt(Rt * Rt - d1 * d1 - d2 * d2), py = d1, pz = d2;
+        dx = -1.0; dy = 0.0; dz = 0.0;
+        px = sqrt(Rt * Rt - d1 * d1 - d2 * d2); py = d1; pz = d2;
         if (R.stellar_direction) {   // ARTES.f90:1080-1111
             double c = cos_b(-(HALF_PI - R.theta_star)), s = sin_b(-(HALF_PI - R.theta_star));
             const double x1 = c * px + s * pz, y1 = py, z1 = -s * px + c * pz;
@@ -473,8 +645,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
             if (pd > TWO_PI) pd -= TWO_PI;
             dx = sin_b(td) * cos_b(pd); dy = sin_b(td) * sin_b(pd); dz = cos_b(td);
         }
-        int cr = G.nr - 1, ct = 0, cp = 0;   // initial_cell (ARTES.f90:2605-2669)
-        if constexpr (G3D) {
+        if constexpr (G3D) {   // initial_cell (ARTES.f90:2605-2669)
             const double r = sqrt(px * px + py * py + pz * pz);
             const double th = acos(pz / r);
             double ph = atan2(py, px);
@@ -486,13 +657,14 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
                 if (ph > G.phif[j] && ph < hi) { cp = j; break; }
             }
         }
+        }   // star
         S.s[slot].pid = pid;
         S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
         S.s[slot].px = px; S.s[slot].py = py; S.s[slot].pz = pz;
         S.s[slot].dx = dx; S.s[slot].dy = dy; S.s[slot].dz = dz;
-        S.s[slot].s0 = 1.0; S.s[slot].s1 = 0.0; S.s[slot].s2 = 0.0; S.s[slot].s3 = 0.0;
-        S.s[slot].wI = 1.0;
-        S.s[slot].pcell = pack_cell(cr, ct, cp); S.s[slot].pface = pack_face(1, G.nr);
+        S.s[slot].s0 = wI; S.s[slot].s1 = 0.0; S.s[slot].s2 = 0.0; S.s[slot].s3 = 0.0;
+        S.s[slot].wI = wI;
+        S.s[slot].pcell = pack_cell(cr, ct, cp); S.s[slot].pface = face;
         S.s[slot].ttgt = 0.0;
         S.s[slot].cs0 = S.s[slot].cs1 = S.s[slot].cs2 = S.s[slot].cs3 = 0.0;
         S.s[slot].pt0 = S.s[slot].pt1 = S.s[slot].pt2 = S.s[slot].pt3 = 0.0;
@@ -500,7 +672,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         S.s[slot].cur_pix = -1;
         S.s[slot].nscat = 0;
         S.s[slot].ncross = 0;
-        S.s[slot].mode = S_FIRST;
+        S.s[slot].mode = mode0;
         }   // emit
         if (i < n) L.trace_out[out0 + i] = emit ? slot : -1;
     }
@@ -516,6 +688,13 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         if (q1 != 0.0) unsafeAtomicAdd(&R.tot2[1], q1);
         if (q2 != 0.0) unsafeAtomicAdd(&R.tot2[2], q2);
         if (q3 != 0.0) unsafeAtomicAdd(&R.tot2[3], q3);
+    }
+    if (R.photon_source == 2) {
+        const double fe = wave_sum_f64(f_emit), fx = wave_sum_f64(f_exit);
+        if ((threadIdx.x & 63) == 0) {
+            if (fe != 0.0) unsafeAtomicAdd(&R.tot2[4], fe);
+            if (fx != 0.0) unsafeAtomicAdd(&R.tot2[5], fx);
+        }
     }
 }
 

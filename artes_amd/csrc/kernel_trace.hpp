@@ -241,7 +241,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     pcell = rec->pcell; pface = rec->pface;
                     ncross = rec->ncross;
                     wI = rec->wI;
-                    const bool peel = (mode == S_PEEL);
+                    const bool peel = is_peel_trace(mode);
                     start_trace(peel ? R.det0 : ldx, peel ? R.det1 : ldy, peel ? R.det2 : ldz);
                     have = true;
                 }
@@ -350,14 +350,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         end = S_END_EXIT;
                     } else {                                       // reached the surface (ARTES.f90:755-774)
                         const double xi = rng.uni();
-                        if (xi > R.surface_albedo) end = S_END_ABS;
-                        else { log_err(R, 62); end = S_END_DROP; }
+                        if (xi > R.surface_albedo) {
+                            end = S_END_ABS;
+                        } else {
+                            // Lambertian reflection: k_event turns the packet at the surface point,
+                            // the propagation then resumes with the optical depth still to go
+                            px = tx + best * nx; py = ty + best * ny; pz = tz + best * nz;
+                            pcell = pack_cell(tcr, tct, tcp);
+                            pface = pack_face(1, G.cell_depth);
+                            ttgt = ttgt - (tacc + tau_cell);
+                            end = S_SURF_HIT;
+                        }
                     }
-                } else {   // S_FIRST or S_PEEL reached the boundary: total optical depth known
+                } else {   // a first-optical-depth or peel-off trace reached the boundary
                     tacc += tau_cell;
-                    if (err) log_err(R, mode == S_FIRST ? 2 : 43);
-                    if (mode == S_PEEL) {
-                        end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0);
+                    // error codes of the four traces (ARTES.f90:640, 4743, 4549, 4653)
+                    if (err) log_err(R, mode == S_FIRST ? 2 : mode == S_PEEL ? 43 : mode == S_PEEL_T ? 46 : 42);
+                    if (is_peel_trace(mode)) {
+                        const int kind = mode == S_PEEL_T ? 1 : mode == S_PEEL_S ? 2 : 0;
+                        end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0) | (kind << PEEL_KIND_SHIFT);
                     } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
                         end = S_END_DROP;
                     } else {
@@ -381,12 +392,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     rec->mode = end; rec->ncross = ncross;
                     rec->wI = wI;
                     rec->tpeel = tacc;
+                    rec->ttgt = ttgt;
                     have = false;
                 }
             }   // pending == 0
         }   // have
-        q_event.push(end && (end & 0xFF) == S_PEEL_DONE, slot, L.event, L.event_n);
-        q_emit.push(end && (end & 0xFF) != S_PEEL_DONE, slot, L.emit, L.emit_n);
+        q_event.push(end && to_event_list(end), slot, L.event, L.event_n);
+        q_emit.push(end && !to_event_list(end), slot, L.emit, L.emit_n);
     }
     q_event.flush(L.event, L.event_n);
     q_emit.flush(L.emit, L.emit_n);

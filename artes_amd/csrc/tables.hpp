@@ -16,6 +16,10 @@
 //   * the cumulative azimuth tables SC2(i) = sum cos2beta, SS2(i) = sum sin2beta
 //     (ARTES.f90:404-420, 1545-1587)
 //   * face tables: rfront^2, tan^2(theta_f), thetaplane, sin/cos(phi_f) (ARTES.f90:2261-2270)
+//   * thermal source (build_thermal): per wavelength the absorption cell_depth, cell
+//     luminosity weights and the emissivity CDF of the planet branch of
+//     grid_initialize(2) (ARTES.f90:2359-2453), laid out in the reference's sampling
+//     order so emit_photon's linear scan (1126-1154) becomes a binary search
 #pragma once
 
 #include <cmath>
@@ -41,6 +45,10 @@ struct HostTables {
     std::vector<double> rfront, rf2, thetaf, tan2, phif, phis, phic;
     std::vector<int32_t> tplane;
     std::vector<double> kappa;     // [nwav][ncell]
+    std::vector<double> kabs;      // [nwav][ncell] absorption (thermal source)
+    std::vector<double> temperature;  // [ncell], empty if not given
+    std::vector<double> wavelength;   // [nwav] m
+    std::vector<double> tcos;      // cos(theta_f) [ntheta+1]
     std::vector<double> albedo;    // [nwav][ncell]
     std::vector<int32_t> matid;    // [nwav][ncell]
     std::vector<double> mats;      // [nmat][180][16]
@@ -81,6 +89,8 @@ inline HostTables build_tables(const artes_grid_desc& d) {
         double tt = std::tan(T.thetaf[i]);
         T.tan2[i] = tt * tt;
     }
+    T.tcos.resize(d.ntheta + 1);
+    for (int i = 0; i <= d.ntheta; i++) T.tcos[i] = std::cos(T.thetaf[i]);   // theta_grid_cos, ARTES.f90:2263
     T.phif.resize(d.nphi); T.phis.resize(d.nphi); T.phic.resize(d.nphi);
     for (int i = 0; i < d.nphi; i++) {          // ARTES.f90:2267-2270
         T.phif[i] = d.phi_deg[i] * pi / 180.0;
@@ -89,6 +99,10 @@ inline HostTables build_tables(const artes_grid_desc& d) {
     }
 
     const size_t nwc = (size_t)d.nwav * T.ncell;
+    T.kabs.assign(d.kappa_abs, d.kappa_abs + nwc);
+    if (d.temperature) T.temperature.assign(d.temperature, d.temperature + T.ncell);
+    T.wavelength.resize(d.nwav);
+    for (int i = 0; i < d.nwav; i++) T.wavelength[i] = d.wavelength_um ? d.wavelength_um[i] * 1.e-6 : 0.0;
     T.kappa.resize(nwc); T.albedo.resize(nwc);
     for (size_t i = 0; i < nwc; i++) {           // ARTES.f90:2178-2188
         double ext = d.kappa_sca[i] + d.kappa_abs[i];
@@ -207,6 +221,74 @@ inline HostTables build_tables(const artes_grid_desc& d) {
         T.cell_depth[wl] = cell_max;
     }
     return T;
+}
+
+// Thermal source of one wavelength (grid_initialize(2), planet branch, ARTES.f90:2359-2453).
+struct ThermalTables {
+    int cell_depth = 0;
+    double total = 0.0;              // emissivity_cumulative(nr-1, ntheta-1, nphi-1) [W m-1]
+    std::vector<double> cdf;         // [(nr - cell_depth) * ntheta * nphi], order (i, j, k), k fastest
+    std::vector<double> weight;      // cell_weight [ncell] (C order [nphi][ntheta][nr])
+    std::vector<double> luminosity;  // cell_luminosity [ncell] [W m-1]
+};
+
+inline ThermalTables build_thermal(const HostTables& T, int wl, bool thermal_weight, bool ring) {
+    if (T.temperature.empty()) throw std::invalid_argument("photon:source=planet needs the temperature array");
+    const double pi = 4.0 * std::atan(1.0);
+    const double k_b = 1.3806488e-23, hh = 6.62606957e-34, cc = 2.99792458e8;   // ARTES.f90:10-13
+    const double lam = T.wavelength[wl];
+    const double* ab = &T.kabs[(size_t)wl * T.ncell];
+    auto cidx = [&](int i, int j, int k) { return ((size_t)k * T.ntheta + j) * T.nr + i; };
+    // planck_function, per steradian (ARTES.f90:1362)
+    auto planck = [&](double t) { return (2.0 * hh * cc * cc / std::pow(lam, 5.0)) / (std::exp(hh * cc / (lam * k_b * t)) - 1.0); };
+    // cell_volume (ARTES.f90:2274-2300)
+    auto volume = [&](int i, int j, int k) {
+        double dphi = 2.0 * pi;
+        if (T.nphi > 1) dphi = (k < T.nphi - 1) ? T.phif[k + 1] - T.phif[k] : 2.0 * pi - T.phif[k];
+        const double r1 = T.rfront[i + 1], r0 = T.rfront[i];
+        return T.oblate_x * T.oblate_y * T.oblate_z * (1.0 / 3.0) * (r1 * r1 * r1 - r0 * r0 * r0) * (T.tcos[j] - T.tcos[j + 1]) * dphi;
+    };
+    ThermalTables X;
+    // deepest cell where the absorption optical depth from the top exceeds 5 (ARTES.f90:2361-2391)
+    int cell_max = 1000000, depth = 0;
+    const int grid_out = ring ? 2 : 0;
+    for (int j = 0; j < T.ntheta; j++)
+        for (int k = 0; k < T.nphi; k++) {
+            double tot = 0.0;
+            for (int i = grid_out; i < T.nr; i++) {
+                tot += ab[cidx(T.nr - i - 1, j, k)] * (T.rfront[T.nr - i] - T.rfront[T.nr - i - 1]);
+                depth = T.nr - i - 1;
+                if (tot > 5.0) break;
+            }
+            if (depth < cell_max) cell_max = depth;
+        }
+    X.cell_depth = cell_max;
+    double norm = 0.0;
+    for (int i = X.cell_depth; i < T.nr; i++)
+        for (int j = 0; j < T.ntheta; j++)
+            for (int k = 0; k < T.nphi; k++) {
+                const size_t c = cidx(i, j, k);
+                if (T.temperature[c] > 0.0) norm += ab[c] * planck(T.temperature[c]) * volume(i, j, k);
+            }
+    X.weight.assign(T.ncell, 0.0);
+    X.luminosity.assign(T.ncell, 0.0);
+    X.cdf.assign((size_t)(T.nr - X.cell_depth) * T.ntheta * T.nphi, 0.0);
+    double total = 0.0;
+    size_t o = 0;
+    for (int i = X.cell_depth; i < T.nr; i++)
+        for (int j = 0; j < T.ntheta; j++)
+            for (int k = 0; k < T.nphi; k++, o++) {
+                const size_t c = cidx(i, j, k);
+                if (T.temperature[c] > 0.0 && ab[c] > 0.0) {
+                    const double b = planck(T.temperature[c]), v = volume(i, j, k);
+                    X.weight[c] = thermal_weight ? norm / (v * ab[c] * b) : 1.0;
+                    X.luminosity[c] = 4.0 * pi * v * ab[c] * b;
+                    total = total + X.luminosity[c] * X.weight[c];
+                }
+                X.cdf[o] = total;
+            }
+    X.total = total;
+    return X;
 }
 
 }  // namespace artes

@@ -33,8 +33,10 @@
 
 namespace artes {
 
-// sum the NCOPY privatised detectors into `out` ([4][4][ny][nx], accumulated) and
-// replicate the peel count into the four Stokes slots of plane 2 (ARTES.f90:4969-4972)
+// sum the NCOPY privatised detectors into `out` ([4][4][ny][nx], accumulated).  Copy
+// plane 8 counts the polarised peels, copy plane 9 the I-only ones (thermal emission,
+// surface): the reference adds the first to the counts of all four Stokes components
+// (ARTES.f90:4969-4972), the second to the count of I alone (4581, 4688)
 __global__ void reduce_detector(const double* __restrict__ copies, size_t stride, size_t plane, double* __restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= stride) return;
@@ -44,12 +46,15 @@ __global__ void reduce_detector(const double* __restrict__ copies, size_t stride
     const size_t slot = i / plane;           // 0..15 = moment*4 + stokes
     if (slot == 8) {
         const size_t pix = i - 8 * plane;
-        out[i] += s;
+        double s9 = 0.0;
+#pragma unroll
+        for (int c = 0; c < NCOPY; c++) s9 += copies[(size_t)c * stride + 9 * plane + pix];
+        out[i] += s + s9;
         out[9 * plane + pix] += s;
         out[10 * plane + pix] += s;
         out[11 * plane + pix] += s;
     } else if (slot == 9 || slot == 10 || slot == 11) {
-        // filled from slot 8
+        // filled from slots 8 and 9
     } else {
         out[i] += s;
     }
@@ -67,6 +72,9 @@ struct artes_grid {
            *d_phic = nullptr, *d_kappa = nullptr, *d_albedo = nullptr, *d_mats = nullptr, *d_cums = nullptr,
            *d_sc2 = nullptr, *d_ss2 = nullptr;
     int *d_tplane = nullptr, *d_matid = nullptr;
+    double *d_rfront = nullptr, *d_tcos = nullptr;
+    double *d_th_cdf = nullptr, *d_th_weight = nullptr;   // thermal tables of the last planet-source call
+    size_t th_cap = 0;
     double* d_copies = nullptr;
     size_t copies_cap = 0;
     double* d_out = nullptr;          // scratch outputs for the host-pointer variant
@@ -144,7 +152,7 @@ extern "C" {
 int32_t artes_abi_version(void) { return ARTES_ABI_VERSION; }
 
 const char* artes_build_info(void) {
-    return "artes_amd transport engine: gfx950 HIP, FP64, persistent state-machine kernel, NCOPY=8";
+    return "artes_amd transport engine: gfx950 HIP, FP64, event engine (k_trace / k_event / k_emit), NCOPY=8";
 }
 
 const char* artes_last_error(void) { return g_last_error.c_str(); }
@@ -160,7 +168,7 @@ void artes_grid_destroy(artes_grid* g) {
     hipSetDevice(g->device);
     void* ptrs[] = {g->d_rf2, g->d_thetaf, g->d_tan2, g->d_phif, g->d_phis, g->d_phic, g->d_kappa, g->d_albedo,
                     g->d_mats, g->d_cums, g->d_sc2, g->d_ss2, g->d_tplane, g->d_matid, g->d_copies, g->d_out,
-                    g->d_tot, g->d_cnt, g->d_err, g->d_rec};
+                    g->d_tot, g->d_cnt, g->d_err, g->d_rec, g->d_rfront, g->d_tcos, g->d_th_cdf, g->d_th_weight};
     for (void* p : ptrs)
         if (p) hipFree(p);
     void* eptrs[] = {g->pool_mem, g->d_lists[0], g->d_lists[1], g->d_event, g->d_emit, g->d_counts, g->d_grab, g->d_next};
@@ -200,7 +208,9 @@ int32_t artes_grid_create(const artes_grid_desc* desc, int32_t device, artes_gri
     HIP_TRY(upload(&g->d_cums, T.cums));
     HIP_TRY(upload(&g->d_sc2, T.sc2));
     HIP_TRY(upload(&g->d_ss2, T.ss2));
-    HIP_TRY(hipMalloc((void**)&g->d_tot, 4 * sizeof(double)));
+    HIP_TRY(upload(&g->d_rfront, T.rfront));
+    HIP_TRY(upload(&g->d_tcos, T.tcos));
+    HIP_TRY(hipMalloc((void**)&g->d_tot, 6 * sizeof(double)));
     HIP_TRY(hipMalloc((void**)&g->d_cnt, ARTES_NUM_COUNTERS * sizeof(unsigned long long)));
     HIP_TRY(hipMalloc((void**)&g->d_err, ARTES_NUM_ERR * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&g->ev0));
@@ -224,6 +234,20 @@ int32_t artes_grid_cell_depth(const artes_grid* g, int32_t wl) {
 }
 
 int32_t artes_grid_num_matrices(const artes_grid* g) { return g ? g->T.nmat : -22; }
+
+int32_t artes_grid_thermal(artes_grid* g, int32_t wl, int32_t thermal_weight, int32_t ring, int32_t* cell_depth,
+                           double* emissivity_total, double* cell_luminosity) {
+    if (!g || wl < 0 || wl >= g->T.nwav) return fail(-22, "bad grid or wavelength index");
+    try {
+        const ThermalTables X = build_thermal(g->T, wl, thermal_weight != 0, ring != 0);
+        if (cell_depth) *cell_depth = X.cell_depth;
+        if (emissivity_total) *emissivity_total = X.total;
+        if (cell_luminosity) std::memcpy(cell_luminosity, X.luminosity.data(), X.luminosity.size() * sizeof(double));
+    } catch (const std::exception& e) {
+        return fail(-22, e.what());
+    }
+    return 0;
+}
 
 }  // extern "C"
 
@@ -299,8 +323,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const size_t ev_bytes = event_table_doubles(G.nmat) * sizeof(double);
     const char* el = getenv("ARTES_EVENT_LDS");
     const bool ev_lds = (el ? atoi(el) != 0 : true) && ev_bytes <= 65536;
-    // detector moments 0-8 accumulated per k_event block in LDS when they fit
-    const size_t det_bytes = 9 * (size_t)R.nx * R.ny * sizeof(double);
+    // detector planes 0-9 accumulated per k_event block in LDS when they fit
+    const size_t det_bytes = 10 * (size_t)R.nx * R.ny * sizeof(double);
     const char* dl = getenv("ARTES_DET_LDS");
     const bool det_lds = (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
     int ev_blocks = side_blocks;
@@ -377,10 +401,11 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
                       double* rec, hipStream_t stream) {
     const HostTables& T = g->T;
     if (!p) return fail(-22, "null params");
-    if (p->photon_source != 1) return fail(-38, "photon:source=planet is not implemented in the GPU engine yet");
+    if (p->photon_source != 1 && p->photon_source != 2) return fail(-22, "photon_source must be 1 (star) or 2 (planet)");
+    if (!use_event_engine() && (p->photon_source != 1 || p->surface_albedo > 0.0))
+        return fail(-38, "the persistent engine supports the star source without surface reflection only");
     if (p->wl_index < 0 || p->wl_index >= T.nwav) return fail(-22, "wl_index out of range");
     if (p->nx < 1 || p->ny < 1 || (size_t)p->nx * p->ny > (1u << 26)) return fail(-22, "bad detector size");
-    if (p->surface_albedo > 0.0) return fail(-38, "planet:surface_albedo > 0 (Lambertian surface) is not implemented yet");
     HIP_TRY(hipSetDevice(g->device));
     const size_t plane = (size_t)p->nx * p->ny;
     const size_t stride = 16 * plane;
@@ -395,6 +420,33 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     DevGrid G;
     G.nr = T.nr; G.ntheta = T.ntheta; G.nphi = T.nphi; G.ncell = T.ncell; G.nmat = T.nmat;
     G.cell_depth = p->cell_depth >= 0 ? p->cell_depth : T.cell_depth[p->wl_index];
+    G.rfr = g->d_rfront; G.tcos = g->d_tcos;
+    G.ox = T.oblate_x; G.oy = T.oblate_y; G.oz = T.oblate_z;
+    G.th_cdf = nullptr; G.th_weight = nullptr; G.th_ncdf = 0; G.th_cd0 = 0; G.th_total = 0.0;
+    if (p->photon_source == 2) {   // thermal tables of this wavelength (ARTES.f90:2359-2453)
+        ThermalTables X;
+        try {
+            X = build_thermal(T, p->wl_index, p->thermal_weight != 0, p->ring != 0);
+        } catch (const std::exception& e) {
+            return fail(-22, e.what());
+        }
+        if (!(X.total > 0.0)) return fail(-22, "planet source: the atmosphere emits nothing at this wavelength");
+        const size_t need = std::max(X.cdf.size(), X.weight.size());
+        if (g->th_cap < need) {
+            if (g->d_th_cdf) hipFree(g->d_th_cdf);
+            if (g->d_th_weight) hipFree(g->d_th_weight);
+            g->d_th_cdf = g->d_th_weight = nullptr;
+            HIP_TRY(hipMalloc((void**)&g->d_th_cdf, need * sizeof(double)));
+            HIP_TRY(hipMalloc((void**)&g->d_th_weight, need * sizeof(double)));
+            g->th_cap = need;
+        }
+        HIP_TRY(hipMemcpyAsync(g->d_th_cdf, X.cdf.data(), X.cdf.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(g->d_th_weight, X.weight.data(), X.weight.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipStreamSynchronize(stream));   // the host vectors go out of scope
+        G.th_cdf = g->d_th_cdf; G.th_weight = g->d_th_weight;
+        G.th_ncdf = (int)X.cdf.size(); G.th_cd0 = X.cell_depth; G.th_total = X.total;
+        if (p->cell_depth < 0) G.cell_depth = X.cell_depth;
+    }
     G.ax2 = 1.0 / (T.oblate_x * T.oblate_x); G.by2 = 1.0 / (T.oblate_y * T.oblate_y); G.cz2 = 1.0 / (T.oblate_z * T.oblate_z);
     G.a = 1.0 / T.oblate_x; G.b = 1.0 / T.oblate_y;
     G.rtop = T.rfront[T.nr];
@@ -408,6 +460,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     DevRun R;
     R.first = first; R.n = n; R.seed = seed;
     R.nx = p->nx; R.ny = p->ny; R.photon_scattering = p->photon_scattering; R.phase_far = p->phase_far;
+    R.photon_source = p->photon_source; R.photon_emission = p->photon_emission; R.photon_bias = p->photon_bias;
     R.stellar_direction = p->stellar_direction;
     const char* env = getenv("ARTES_DEFER");
     R.defer = env ? atoi(env) : 16;
@@ -461,7 +514,7 @@ int32_t artes_run_device(artes_grid* g, const artes_run_params* p, uint64_t firs
     if (!g || !det_dev) return fail(-22, "null argument");
     HIP_TRY(hipSetDevice(g->device));
     hipStream_t s = (hipStream_t)stream;
-    if (!tot_dev) { HIP_TRY(hipMemsetAsync(g->d_tot, 0, 4 * sizeof(double), s)); }
+    if (!tot_dev) { HIP_TRY(hipMemsetAsync(g->d_tot, 0, 6 * sizeof(double), s)); }
     if (!cnt_dev) { HIP_TRY(hipMemsetAsync(g->d_cnt, 0, ARTES_NUM_COUNTERS * 8, s)); }
     if (!err_dev) { HIP_TRY(hipMemsetAsync(g->d_err, 0, ARTES_NUM_ERR * 8, s)); }
     return launch(g, p, first, n, seed, det_dev, tot_dev ? tot_dev : g->d_tot,
@@ -490,7 +543,7 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
         HIP_TRY(hipMemset(g->d_rec, 0, std::max<uint64_t>(n, 1) * 4 * sizeof(double)));
     }
     HIP_TRY(hipMemset(g->d_out, 0, stride * sizeof(double)));
-    HIP_TRY(hipMemset(g->d_tot, 0, 4 * sizeof(double)));
+    HIP_TRY(hipMemset(g->d_tot, 0, 6 * sizeof(double)));
     HIP_TRY(hipMemset(g->d_cnt, 0, ARTES_NUM_COUNTERS * 8));
     HIP_TRY(hipMemset(g->d_err, 0, ARTES_NUM_ERR * 8));
     int32_t rc = launch(g, p, first, n, seed, g->d_out, g->d_tot, g->d_cnt, g->d_err, records ? g->d_rec : nullptr, 0);
@@ -500,7 +553,7 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
     HIP_TRY(hipMemcpy(hd.data(), g->d_out, stride * sizeof(double), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < stride; i++) det[i] += hd[i];
     if (totals) {
-        double t2[4];
+        double t2[6];
         HIP_TRY(hipMemcpy(t2, g->d_tot, sizeof(t2), hipMemcpyDeviceToHost));
         const size_t plane = (size_t)p->nx * p->ny;
         for (int k = 0; k < 4; k++) {
@@ -509,6 +562,8 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
             totals[k] += s;
             totals[4 + k] += t2[k];
         }
+        totals[8] += t2[4];   // flux_emitted
+        totals[9] += t2[5];   // flux_exit
     }
     if (counters) {
         unsigned long long c[ARTES_NUM_COUNTERS];

@@ -265,7 +265,9 @@ def run_params(cfg: RunConfig, det: Detector, wl_index: int = 0, det_phi: float 
         stellar_direction=int(bool(cfg.stellar_direction)), cell_depth=int(cell_depth),
         det_theta=float(det.det_theta), det_phi=float(phi), x_max=float(det.x_max), y_max=float(det.y_max),
         fstop=float(cfg.fstop), photon_minimum=float(cfg.photon_minimum), surface_albedo=float(cfg.surface_albedo),
-        theta_star=float(cfg.theta_star), phi_star=float(cfg.phi_star))
+        theta_star=float(cfg.theta_star), phi_star=float(cfg.phi_star),
+        photon_emission=int(cfg.photon_emission), thermal_weight=int(bool(cfg.thermal_weight)),
+        ring=int(bool(cfg.ring)), reserved=0, photon_bias=float(cfg.photon_bias))
 
 
 def default_config() -> RunConfig:

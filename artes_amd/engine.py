@@ -12,7 +12,8 @@ import os
 
 import numpy as np
 
-from .abi import ARTES_NUM_COUNTERS, ARTES_NUM_ERR, COUNTER_NAMES, GridArrays, GridDesc, RunParams
+from .abi import (ARTES_ABI_VERSION, ARTES_NUM_COUNTERS, ARTES_NUM_ERR, ARTES_NUM_TOTALS, COUNTER_NAMES, GridArrays,
+                  GridDesc, RunParams)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ARTES_LIB_PATH") or os.path.join(HERE, "lib", "libartes_hip.so")
@@ -54,6 +55,9 @@ def lib():
     L.artes_grid_destroy.argtypes = [C.c_void_p]
     L.artes_grid_cell_depth.restype = C.c_int32
     L.artes_grid_cell_depth.argtypes = [C.c_void_p, C.c_int32]
+    L.artes_grid_thermal.restype = C.c_int32
+    L.artes_grid_thermal.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
+                                     C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.artes_grid_num_matrices.restype = C.c_int32
     L.artes_grid_num_matrices.argtypes = [C.c_void_p]
     dp, up = C.POINTER(C.c_double), C.POINTER(C.c_uint64)
@@ -70,7 +74,7 @@ def lib():
     L.artes_set_profiling.argtypes = [C.c_void_p, C.c_int32]
     L.artes_kernel_times.restype = C.c_int32
     L.artes_kernel_times.argtypes = [C.c_void_p, dp, up]
-    if L.artes_abi_version() != 1:
+    if L.artes_abi_version() != ARTES_ABI_VERSION:
         raise EngineUnavailable("ABI version mismatch")
     _lib = L
     return L
@@ -90,7 +94,7 @@ class RunResult:
 
     def __init__(self, det, totals, counters, err):
         self.det = det            # [4][4][ny][nx]
-        self.totals = totals      # [8]
+        self.totals = totals      # [ARTES_NUM_TOTALS]
         self.counters = counters  # [ARTES_NUM_COUNTERS]
         self.err = err            # [ARTES_NUM_ERR]
 
@@ -125,12 +129,22 @@ class Grid:
     def cell_depth(self, wl: int = 0) -> int:
         return lib().artes_grid_cell_depth(self.h, wl)
 
+    def thermal(self, wl: int = 0, thermal_weight: bool = True, ring: bool = False):
+        """Thermal-source tables (``artes_grid_thermal``): (cell_depth, emissivity_total,
+        cell_luminosity[nphi][ntheta][nr])."""
+        cd = C.c_int32()
+        tot = C.c_double()
+        lum = np.zeros((self.nphi, self.ntheta, self.nr))
+        _check(lib().artes_grid_thermal(self.h, int(wl), int(bool(thermal_weight)), int(bool(ring)), C.byref(cd),
+                                        C.byref(tot), lum.ctypes.data_as(C.POINTER(C.c_double))), "artes_grid_thermal")
+        return cd.value, tot.value, lum
+
     def num_matrices(self) -> int:
         return lib().artes_grid_num_matrices(self.h)
 
     def run(self, params: RunParams, first: int, n: int, seed: int) -> RunResult:
         det = np.zeros((4, 4, params.ny, params.nx))
-        tot = np.zeros(8)
+        tot = np.zeros(ARTES_NUM_TOTALS)
         cnt = np.zeros(ARTES_NUM_COUNTERS, dtype=np.uint64)
         err = np.zeros(ARTES_NUM_ERR, dtype=np.uint64)
         dp, up = C.POINTER(C.c_double), C.POINTER(C.c_uint64)

@@ -31,8 +31,8 @@ def per_packet_pixel_variance(raw: np.ndarray, n_packets: int) -> np.ndarray:
 
 
 def total_sigma_raw(totals: np.ndarray, n_packets: int) -> np.ndarray:
-    """Honest sigma of the integrated sums per Stokes (raw units) from totals[8]."""
-    t1, t2 = totals[:4], totals[4:]
+    """Honest sigma of the integrated sums per Stokes (raw units) from totals[0:8]."""
+    t1, t2 = totals[:4], totals[4:8]
     return np.sqrt(np.clip(t2 - t1 * t1 / float(n_packets), 0.0, None))
 
 

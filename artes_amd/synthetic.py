@@ -74,3 +74,21 @@ def make_config(name: str, **over) -> dict:
     spec = dict(CONFIGS[name])
     spec.update(over)
     return make(**spec)
+
+
+def make_thermal(kind: str = "ray", nr: int = 16, ntheta: int = 8, nphi: int = 8, tau_abs: float = 1.0,
+                 tau_sca: float = 1.0, temperature=1000.0, height: float = 100e3, radius: float = R_JUP,
+                 wavelength=(10.0,), **kw) -> dict:
+    """A thermally emitting atmosphere (``photon:source=planet``): uniform absorption and
+    scattering of radial optical depths ``tau_abs`` / ``tau_sca`` and a temperature that is
+    either a constant or a callable of the cell-centre radius [m] (e.g. a lapse rate)."""
+    atm = make(kind=kind, nr=nr, ntheta=ntheta, nphi=nphi, tau=1.0, height=height, radius=radius,
+               wavelength=wavelength, **kw)
+    shape = atm["temperature"].shape
+    nwav = len(wavelength)
+    atm["absorption"] = np.full((nwav,) + shape, tau_abs / height)
+    atm["scattering"] = np.full((nwav,) + shape, tau_sca / height)
+    rc = 0.5 * (atm["radial"][1:] + atm["radial"][:-1])
+    t = temperature(rc) if callable(temperature) else np.full(nr, float(temperature))
+    atm["temperature"] = np.broadcast_to(np.asarray(t, dtype=np.float64)[None, None, :], shape).copy()
+    return atm

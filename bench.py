@@ -85,7 +85,7 @@ def main() -> int:
 
     f64 = dict(dtype=torch.float64, device=f"cuda:{dev}")
     det = torch.zeros((4, 4, ny, nx), **f64)
-    tot2 = torch.zeros(4, **f64)
+    tot2 = torch.zeros(6, **f64)   # sum T^2 per Stokes, flux_emitted, flux_exit (include/artes_amd.h)
     cnt = torch.zeros(8, dtype=torch.int64, device=f"cuda:{dev}")
     err = torch.zeros(64, dtype=torch.int64, device=f"cuda:{dev}")
     stream = torch.cuda.current_stream()

@@ -23,8 +23,13 @@
  *     same pixel, so the per-peel sum w^2 underestimates it by ~1.7-3x).  Values
  *     are in units of packet weight; the caller multiplies by package_energy
  *     (ARTES.f90:964-970).
- *   - totals[8]: sum_p T_p and sum_p T_p^2 of each packet's total detected weight
- *     T_p per Stokes component (honest variance of the integrated photometry).
+ *   - totals[ARTES_NUM_TOTALS]: [0..3] sum_p T_p and [4..7] sum_p T_p^2 of each
+ *     packet's total detected weight T_p per Stokes component (honest variance of
+ *     the integrated photometry); [8] flux_emitted and [9] flux_exit of the thermal
+ *     source (ARTES.f90:607, 780, 953), in units of packet weight.
+ *   - Peels that carry Stokes I only (thermal emission, ARTES.f90:4519-4598;
+ *     Lambertian surface, 4600-4708) add their count to the Stokes-I count alone,
+ *     as the reference does.
  *   - Functions return 0 on success or a negative errno-style code; they never
  *     exit the process (the reference calls exit(0) on fatal errors).
  *   - Error-code counters: uint64_t err[ARTES_NUM_ERR], index = the reference's
@@ -40,7 +45,8 @@
 extern "C" {
 #endif
 
-#define ARTES_ABI_VERSION 1
+#define ARTES_ABI_VERSION 2
+#define ARTES_NUM_TOTALS 10
 #define ARTES_NUM_ERR 64
 
 /* Counter slots (uint64_t counters[ARTES_NUM_COUNTERS]). */
@@ -75,17 +81,23 @@ typedef struct artes_grid_desc {
 typedef struct artes_run_params {
     int32_t wl_index;        /* 0-based wavelength (wl_count-1)                    */
     int32_t nx, ny;          /* detector pixels (1x1 for spectrum/phase)           */
-    int32_t photon_source;   /* 1 = star (2 = planet: not yet supported -> -ENOSYS) */
+    int32_t photon_source;   /* 1 = star, 2 = planet (thermal emission)            */
     int32_t photon_scattering; /* photon:scattering on/off                         */
     int32_t phase_far;       /* phase_curve && det_phi >= 170 deg (ARTES.f90:1041) */
     int32_t stellar_direction; /* star:direction (ARTES.f90:1080-1111)             */
-    int32_t cell_depth;      /* surface face index; <0 => computed (ARTES.f90:2329) */
+    int32_t cell_depth;      /* surface face index; <0 => computed (ARTES.f90:2329-2392) */
     double det_theta, det_phi; /* detector direction [rad], already clamped       */
     double x_max, y_max;     /* image half-size [m] (ARTES.f90:475-479)            */
     double fstop;            /* photon:fstop                                        */
     double photon_minimum;   /* photon:minimum                                      */
     double surface_albedo;   /* planet:surface_albedo                               */
     double theta_star, phi_star; /* stellar direction [rad]                         */
+    /* thermal source (photon:source=planet), ARTES.f90:1117-1266, 2359-2453 */
+    int32_t photon_emission; /* 1 = isotropic, 2 = biased upward (photon:emission)  */
+    int32_t thermal_weight;  /* photon:weight: cell luminosity weighting on/off     */
+    int32_t ring;            /* planet:ring (thermal cell_depth skips 2 cells)      */
+    int32_t reserved;
+    double photon_bias;      /* photon:bias, 0 <= b < 1                             */
 } artes_run_params;
 
 typedef struct artes_grid artes_grid;
@@ -107,6 +119,16 @@ void    artes_grid_destroy(artes_grid* grid);
 /* cell_depth for a wavelength (grid_initialize(2), ARTES.f90:2329-2357). */
 int32_t artes_grid_cell_depth(const artes_grid* grid, int32_t wl_index);
 
+/* Thermal source tables of one wavelength (grid_initialize(2), planet branch,
+ * ARTES.f90:2359-2453, with cell_volume 2274-2300 and planck_function 1350-1367):
+ * cell_depth (absorption optical depth 5 from the top; `ring` skips the two outer
+ * cells), the total weighted emissivity emissivity_cumulative(nr-1,ntheta-1,nphi-1)
+ * [W m-1] that sets package_energy (2535), and optionally cell_luminosity
+ * [nphi][ntheta][nr] [W m-1] (the cell_luminosity.fits of write_output, 3658).
+ * Needs the temperature array in artes_grid_desc. */
+int32_t artes_grid_thermal(artes_grid* grid, int32_t wl_index, int32_t thermal_weight, int32_t ring,
+                           int32_t* cell_depth, double* emissivity_total, double* cell_luminosity);
+
 /* Number of distinct (cell, wavelength) scattering matrices kept after dedup. */
 int32_t artes_grid_num_matrices(const artes_grid* grid);
 
@@ -115,7 +137,7 @@ int32_t artes_grid_num_matrices(const artes_grid* grid);
  * results do not depend on how packets are sharded).  Synchronous; host outputs,
  * all ACCUMULATED into (so shards/wavelengths can be summed in place):
  *   detector   [4][4][ny][nx]   (see Conventions)
- *   totals     [8]              (may be NULL)
+ *   totals     [ARTES_NUM_TOTALS] (may be NULL)
  *   counters   [ARTES_NUM_COUNTERS] (may be NULL)
  *   err        [ARTES_NUM_ERR]  (may be NULL)
  * Replaces radiative_transfer's packet loop + thread reduction (ARTES.f90:546-975). */
@@ -126,7 +148,8 @@ int32_t artes_run(artes_grid* grid, const artes_run_params* params,
 /* Device variant: outputs are DEVICE pointers (e.g. torch tensors) accumulated
  * into on `stream` (a hipStream_t, NULL = default stream), so the caller can
  * all-reduce `detector_dev` with RCCL on the same stream.  totals_dev holds only
- * the four sum_p T_p^2 values (the sums T_p are the detector plane-0 totals).
+ * the four sum_p T_p^2 values (the sums T_p are the detector plane-0 totals)
+ * followed by flux_emitted and flux_exit: totals_dev[6].
  * The event engine polls its live-packet count from the host every few
  * iterations, so the call returns once the transport has drained; the final
  * detector reduction is still in flight on `stream`. */

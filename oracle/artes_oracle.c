@@ -26,7 +26,13 @@
  *   - A packet whose cell_face reports cell_error is dropped immediately; the
  *     reference keeps stepping with undefined cell indices before dropping it.
  *   - error.log lines become counters err[NNN].
- * Only the star source (photon:source=star) is restated; see DESIGN.md §8f.
+ * Thermal emission (photon:source=planet: emit_photon 1117-1266, peel_thermal
+ * 4519-4598, grid_initialize(2) 2359-2453) and the Lambertian surface (lambertian
+ * 1369-1402, peel_surface 4600-4708) are restated too.  The reference's frozen runs
+ * cover only the star source, so these two are pinned by analytic known answers
+ * alone (tests/test_oracle_thermal.py): parity with the reference is unpinned there.
+ * peel_surface keeps stepping after a cell_error (error 042) in the reference; here
+ * that peel is abandoned, like every other trace with a cell_error.
  */
 #include <math.h>
 #include <stdint.h>
@@ -77,6 +83,9 @@ typedef struct oracle_grid {
     int* thetaplane;
     double* cell_opacity;   /* [nwav][ncell] */
     double* cell_albedo;    /* [nwav][ncell] */
+    double* cell_abs;       /* [nwav][ncell] absorption opacity (thermal source) */
+    double* temperature;    /* [ncell] or NULL */
+    double* wavelength;     /* [nwav] m */
     double* p1j_int;        /* [nwav][ncell][4] */
     const double* scatter;  /* raw [180][16][nwav][ncell] */
     double oblate_x, oblate_y, oblate_z;
@@ -96,6 +105,10 @@ typedef struct ctx {
     int cur_pix;           /* pixel of the packet's running contribution (-1: none) */
     double cur_sum[4];     /* running contribution of this packet to cur_pix */
     double pkt_tot[4];     /* this packet's total detected weight */
+    const double* th_cdf;  /* thermal: emissivity CDF in the reference's loop order (i>=cell_depth, j, k) */
+    const double* th_weight; /* thermal: cell_weight [ncell] */
+    double th_total;
+    int th_cd0;            /* thermal: radial index of the first CDF entry (the computed cell_depth) */
 } ctx;
 
 static inline int cidx(const oracle_grid* g, const int c[3]) { return (c[2] * g->ntheta + c[1]) * g->nr + c[0]; }
@@ -157,6 +170,15 @@ oracle_grid* oracle_grid_create(const artes_grid_desc* d) {
         if (alb < 1.e-20) alb = 1.e-20;
         g->cell_albedo[i] = alb;
     }
+    g->cell_abs = (double*)malloc(sizeof(double) * n);
+    for (size_t i = 0; i < n; i++) g->cell_abs[i] = d->kappa_abs[i];
+    g->temperature = NULL;
+    if (d->temperature) {
+        g->temperature = (double*)malloc(sizeof(double) * g->ncell);
+        for (int i = 0; i < g->ncell; i++) g->temperature[i] = d->temperature[i];
+    }
+    g->wavelength = (double*)malloc(sizeof(double) * g->nwav);
+    for (int i = 0; i < g->nwav; i++) g->wavelength[i] = d->wavelength_um[i] * 1.e-6;
     g->scatter = d->scatter;
     for (int m = 0; m < g->nwav; m++)                      /* ARTES.f90:2215-2230 */
         for (int n1 = 1; n1 <= 180; n1++)
@@ -176,6 +198,7 @@ void oracle_grid_destroy(oracle_grid* g) {
     free(g->rfront); free(g->thetafront); free(g->theta_grid_cos); free(g->theta_grid_tan);
     free(g->thetaplane); free(g->phifront); free(g->phi_grid_sin); free(g->phi_grid_cos);
     free(g->cell_opacity); free(g->cell_albedo); free(g->p1j_int);
+    free(g->cell_abs); free(g->temperature); free(g->wavelength);
     free(g);
 }
 
@@ -194,6 +217,79 @@ int oracle_cell_depth(const oracle_grid* g, int wl) {
             if (cell_depth < cell_max) cell_max = cell_depth;
         }
     return cell_max;
+}
+
+/* planck_function, planet source [W m-2 m-1 sr-1] (ARTES.f90:1350-1367) */
+static double planck_sr(double wl, double t) {
+    const double k_b = 1.3806488e-23, hh = 6.62606957e-34, cc = 2.99792458e8;   /* ARTES.f90:10-13 */
+    return (2.0 * hh * cc * cc / pow(wl, 5.0)) / (exp(hh * cc / (wl * k_b * t)) - 1.0);
+}
+
+/* cell_volume (ARTES.f90:2274-2300) */
+static double cell_volume(const oracle_grid* g, int i, int j, int k) {
+    const double pi = PI_;
+    double dphi;
+    if (g->nphi == 1) dphi = 2.0 * pi;
+    else if (k < g->nphi - 1) dphi = g->phifront[k + 1] - g->phifront[k];
+    else dphi = 2.0 * pi - g->phifront[k];
+    const double r1 = g->rfront[i + 1], r0 = g->rfront[i];
+    return g->oblate_x * g->oblate_y * g->oblate_z * (1.0 / 3.0) * (r1 * r1 * r1 - r0 * r0 * r0) *
+           (g->theta_grid_cos[j] - g->theta_grid_cos[j + 1]) * dphi;
+}
+
+/* grid_initialize(2), planet branch (ARTES.f90:2359-2453).  Outputs: cell_depth, the total
+ * weighted emissivity, and (optional) cell_luminosity / cell_weight [ncell] and the CDF in
+ * the reference's loop order (i from cell_depth, then j, then k fastest). */
+int oracle_thermal(const oracle_grid* g, int wl, int thermal_weight, int ring, int* cell_depth_out, double* total_out,
+                   double* lum, double* weight, double* cdf) {
+    const double pi = PI_;
+    if (!g->temperature) return -22;
+    const double* ab = g->cell_abs + (size_t)wl * g->ncell;
+    const double lam = g->wavelength[wl];
+    int cell_max = 1000000, cell_depth = 0;
+    const int grid_out = ring ? 2 : 0;
+    for (int j = 0; j < g->ntheta; j++)
+        for (int k = 0; k < g->nphi; k++) {
+            double tot = 0.0;
+            for (int i = grid_out; i < g->nr; i++) {
+                int c[3] = {g->nr - i - 1, j, k};
+                tot += ab[cidx(g, c)] * (g->rfront[g->nr - i] - g->rfront[g->nr - i - 1]);
+                cell_depth = g->nr - i - 1;
+                if (tot > 5.0) break;
+            }
+            if (cell_depth < cell_max) cell_max = cell_depth;
+        }
+    cell_depth = cell_max;
+    double weight_norm = 0.0;
+    for (int i = cell_depth; i < g->nr; i++)
+        for (int j = 0; j < g->ntheta; j++)
+            for (int k = 0; k < g->nphi; k++) {
+                int c[3] = {i, j, k};
+                const int q = cidx(g, c);
+                if (g->temperature[q] > 0.0) weight_norm += ab[q] * planck_sr(lam, g->temperature[q]) * cell_volume(g, i, j, k);
+            }
+    double total = 0.0;
+    size_t o = 0;
+    if (lum) for (int q = 0; q < g->ncell; q++) lum[q] = 0.0;
+    if (weight) for (int q = 0; q < g->ncell; q++) weight[q] = 0.0;
+    for (int i = cell_depth; i < g->nr; i++)
+        for (int j = 0; j < g->ntheta; j++)
+            for (int k = 0; k < g->nphi; k++, o++) {
+                int c[3] = {i, j, k};
+                const int q = cidx(g, c);
+                if (g->temperature[q] > 0.0 && ab[q] > 0.0) {
+                    const double b = planck_sr(lam, g->temperature[q]), v = cell_volume(g, i, j, k);
+                    const double w = thermal_weight ? weight_norm / (v * ab[q] * b) : 1.0;
+                    const double l = 4.0 * pi * v * ab[q] * b;
+                    if (lum) lum[q] = l;
+                    if (weight) weight[q] = w;
+                    total = total + l * w;
+                }
+                if (cdf) cdf[o] = total;
+            }
+    *cell_depth_out = cell_depth;
+    *total_out = total;
+    return 0;
 }
 
 /* ------------------------------------------------------- geometry -------- */
@@ -673,6 +769,165 @@ static void peel_photon(ctx* X, double xp, double yp, double zp, const double st
     }
 }
 
+/* an I-only peel contribution (peel_thermal / peel_surface, ARTES.f90:4577-4583, 4684-4690) */
+static void add_peel_I(ctx* X, double xp, double yp, double zp, double v, int err_code) {
+    if (!(v > 0.0 && v < 1.e100)) { error_log(X, err_code); return; }
+    double x_im = yp * X->cos_det_phi - xp * X->sin_det_phi;
+    double y_im = zp * X->sin_det_theta - yp * X->cos_det_theta * X->sin_det_phi - xp * X->cos_det_theta * X->cos_det_phi;
+    int ix = (int)((double)X->nx * (x_im + X->p->x_max) / (2.0 * X->p->x_max));
+    int iy = (int)((double)X->ny * (y_im + X->p->y_max) / (2.0 * X->p->y_max));
+    if (ix < 0 || ix >= X->nx || iy < 0 || iy >= X->ny) { error_log(X, 63); return; }
+    size_t plane = (size_t)X->nx * X->ny, pix = (size_t)iy * X->nx + ix;
+    X->detector[0 * plane + pix] += v;
+    X->detector[4 * plane + pix] += v * v;
+    X->detector[8 * plane + pix] += 1.0;
+    X->pkt_tot[0] += v;
+    if ((int)pix != X->cur_pix) {
+        flush_pixel(X);
+        X->cur_pix = (int)pix;
+    }
+    X->cur_sum[0] += v;
+    X->cnt[ARTES_CNT_DETECTED]++;
+    X->peel_sum += v;
+}
+
+/* optical depth from (xp,yp,zp) along the detector direction to the grid boundary or the
+ * surface (the trace loop of peel_thermal / peel_surface); returns 1 if the boundary was
+ * reached, 0 at the surface, -1 on a cell_error (logged as `err_code`) */
+static int peel_depth(ctx* X, double xp, double yp, double zp, const int cell_in[3], const int face_in[2], int err_code,
+                      double* tau_total) {
+    const double* det = X->det;
+    double x = xp, y = yp, z = zp, fd;
+    int cf[2] = {face_in[0], face_in[1]}, nf[2], cell[3] = {cell_in[0], cell_in[1], cell_in[2]}, cout[3], gexit = 0, cerr = 0;
+    *tau_total = 0.0;
+    for (;;) {
+        cell_face(X, x, y, z, det, cf, nf, &fd, &gexit, cell, cout, &cerr);
+        if (cerr) { error_log(X, err_code); return -1; }
+        *tau_total += fd * kappa(X, cell);
+        x += fd * det[0]; y += fd * det[1]; z += fd * det[2];
+        if (gexit) return 1;
+        if (nf[0] == 1 && nf[1] == X->cell_depth) return 0;
+        cf[0] = nf[0]; cf[1] = nf[1];
+        cell[0] = cout[0]; cell[1] = cout[1]; cell[2] = cout[2];
+    }
+}
+
+/* peel_thermal (ARTES.f90:4519-4598); returns nonzero on a cell_error */
+static int peel_thermal(ctx* X, const double pos[3], const double st[4], const int cell[3], const int face[2]) {
+    const double pi = PI_;
+    double tau;
+    int r = peel_depth(X, pos[0], pos[1], pos[2], cell, face, 46, &tau);
+    if (r < 0) return 1;
+    if (r == 1 && tau < 50.0) add_peel_I(X, pos[0], pos[1], pos[2], exp(-tau) / (4.0 * pi) * st[0], 51);
+    return 0;
+}
+
+static void cartesian_spherical(double x, double y, double z, double* r, double* th, double* ph) {
+    const double pi = PI_;
+    *r = sqrt(x * x + y * y + z * z);
+    *th = acos(z / *r);
+    *ph = atan2(y, x);
+    if (*ph < 0.0) *ph += 2.0 * pi;
+}
+
+/* outward unit normal of the (oblate) surface at a point (ARTES.f90:1378-1384) */
+static void surface_normal(const ctx* X, const double pos[3], double nrm[3]) {
+    const oracle_grid* g = X->g;
+    nrm[0] = pos[0] / (g->oblate_x * g->oblate_x);
+    nrm[1] = pos[1] / (g->oblate_y * g->oblate_y);
+    nrm[2] = pos[2] / (g->oblate_z * g->oblate_z);
+    double norm = sqrt(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2]);
+    nrm[0] /= norm; nrm[1] /= norm; nrm[2] /= norm;
+}
+
+/* peel_surface (ARTES.f90:4600-4708): cell_in is the cell below the surface */
+static void peel_surface(ctx* X, const double pos[3], const double st[4], const int cell_in[3], const int face_in[2]) {
+    const double pi = PI_;
+    double nrm[3], rd, td, pd, rn, tn, pn;
+    surface_normal(X, pos, nrm);
+    cartesian_spherical(X->det[0], X->det[1], X->det[2], &rd, &td, &pd);
+    cartesian_spherical(nrm[0], nrm[1], nrm[2], &rn, &tn, &pn);
+    double cos_angle = sin(td) * cos(pd) * sin(tn) * cos(pn) + sin(td) * sin(pd) * sin(tn) * sin(pn) + cos(td) * cos(tn);
+    if (!(cos_angle > 0.0)) return;
+    int cell[3] = {cell_in[0] + 1, cell_in[1], cell_in[2]};
+    double tau;
+    int r = peel_depth(X, pos[0], pos[1], pos[2], cell, face_in, 42, &tau);
+    if (r == 1 && tau < 50.0) add_peel_I(X, pos[0], pos[1], pos[2], exp(-tau) * cos_angle / pi * st[0], 52);
+}
+
+/* lambertian (ARTES.f90:1369-1402): new direction; Stokes becomes (I, 0, 0, 0) */
+static void lambertian(ctx* X, rng_t* rng, const double pos[3], double st[4], double dir[3]) {
+    const double pi = PI_;
+    double nrm[3];
+    surface_normal(X, pos, nrm);
+    double xi = rng_uniform(rng);
+    double alpha = sqrt(xi);
+    xi = rng_uniform(rng);
+    double beta = 2.0 * pi * xi;
+    double dnew[3];
+    direction_cosine(X, alpha, beta, nrm, dnew);
+    dir[0] = dnew[0]; dir[1] = dnew[1]; dir[2] = dnew[2];
+    st[1] = 0.0; st[2] = 0.0; st[3] = 0.0;
+}
+
+/* emit_photon, planet branch (ARTES.f90:1117-1266) */
+static void emit_planet(ctx* X, rng_t* rng, double pos[3], double dir[3], int face[2], int cell[3], double* bias_weight) {
+    const oracle_grid* g = X->g;
+    const artes_run_params* p = X->p;
+    const double pi = PI_;
+    face[0] = 0; face[1] = 0;
+    *bias_weight = 1.0;
+    double xi = rng_uniform(rng);
+    double samp = xi * X->th_total, prev = 0.0;
+    int found = 0;
+    size_t o = 0;
+    cell[0] = X->th_cd0; cell[1] = 0; cell[2] = 0;
+    for (int i = X->th_cd0; i < g->nr && !found; i++)
+        for (int j = 0; j < g->ntheta && !found; j++)
+            for (int k = 0; k < g->nphi; k++, o++) {
+                if (samp >= prev && samp <= X->th_cdf[o]) { cell[0] = i; cell[1] = j; cell[2] = k; found = 1; break; }
+                prev = X->th_cdf[o];
+            }
+    xi = rng_uniform(rng);
+    double r = g->rfront[cell[0]] + xi * (g->rfront[cell[0] + 1] - g->rfront[cell[0]]);
+    xi = rng_uniform(rng);
+    double ct = g->theta_grid_cos[cell[1]] + xi * (g->theta_grid_cos[cell[1] + 1] - g->theta_grid_cos[cell[1]]);
+    double st_ = sqrt(1.0 - ct * ct);
+    double ph;
+    xi = rng_uniform(rng);
+    if (g->nphi == 1) ph = 2.0 * pi * xi;
+    else if (cell[2] < g->nphi - 1) ph = g->phifront[cell[2]] + xi * (g->phifront[cell[2] + 1] - g->phifront[cell[2]]);
+    else ph = g->phifront[cell[2]] + xi * (2.0 * pi - g->phifront[cell[2]]);
+    double cp = cos(ph), sp = sqrt(1.0 - cp * cp);
+    if (ph > pi) sp = -sp;
+    pos[0] = g->oblate_x * (r * st_ * cp);
+    pos[1] = g->oblate_y * (r * st_ * sp);
+    pos[2] = g->oblate_z * (r * ct);
+    if (p->photon_emission == 2) {                  /* biased upward (Gordon 1987), ARTES.f90:1238-1254 */
+        const double b = p->photon_bias;
+        xi = rng_uniform(rng);
+        double yb = (1.0 + b) * tan(pi * xi / 2.0) / sqrt(1.0 - b * b);
+        double ths = acos((1.0 - yb * yb) / (1.0 + yb * yb));
+        xi = rng_uniform(rng);
+        double beta = 2.0 * pi * xi;
+        double nrm[3];
+        surface_normal(X, pos, nrm);
+        direction_cosine(X, cos(pi - ths), beta, nrm, dir);
+        *bias_weight = (pi * sin(ths) * (1.0 + b * cos(ths))) / (2.0 * sqrt(1.0 - b * b));
+    } else {                                        /* isotropic, ARTES.f90:1218-1231 */
+        xi = rng_uniform(rng);
+        double alpha = 2.0 * xi - 1.0;
+        xi = rng_uniform(rng);
+        double beta = 2.0 * pi * xi;
+        double cb = cos(beta), sb = sqrt(1.0 - cb * cb);
+        if (beta > pi) sb = -sb;
+        dir[0] = sqrt(1.0 - alpha * alpha) * cb;
+        dir[1] = sqrt(1.0 - alpha * alpha) * sb;
+        dir[2] = alpha;
+    }
+    if (fabs(dir[2]) >= 1.0) error_log(X, 54);
+}
+
 /* initial_cell (ARTES.f90:2605-2669), star branch */
 static void initial_cell(const ctx* X, double x, double y, double z, int cell[3]) {
     const oracle_grid* g = X->g;
@@ -731,13 +986,14 @@ static void emit_star(ctx* X, rng_t* rng, double pos[3], double dir[3], int face
     initial_cell(X, pos[0], pos[1], pos[2], cell);
 }
 
-/* propagation to the next interaction (ARTES.f90:689-778 / 848-941).
+/* propagation to the next interaction (ARTES.f90:689-778 / 848-941), with the surface:
+ * absorption with probability 1 - surface_albedo, else Lambertian reflection and its peel
+ * (ARTES.f90:753-774, 922-937); the optical depth keeps accumulating after a reflection.
  * returns 0 = interaction reached, 1 = grid exit, 2 = surface absorbed, 3 = cell error */
-static int propagate(ctx* X, rng_t* rng, double pos[3], const double dir[3], int face[2], int cell[3], double tau,
+static int propagate(ctx* X, rng_t* rng, double pos[3], double dir[3], int face[2], int cell[3], double tau,
                      double st[4]) {
     double fd, tau_run = 0.0;
     int nf[2], cout[3], gexit, cerr;
-    (void)st;
     for (;;) {
         cell_face(X, pos[0], pos[1], pos[2], dir, face, nf, &fd, &gexit, cell, cout, &cerr);
         if (cerr) { error_log(X, 3); return 3; }
@@ -756,9 +1012,10 @@ static int propagate(ctx* X, rng_t* rng, double pos[3], const double dir[3], int
         if (nf[0] == 1 && nf[1] == X->cell_depth) {
             double xi = rng_uniform(rng);
             if (xi > X->p->surface_albedo) return 2;
-            /* Lambertian reflection (surface_albedo > 0) is not restated: DESIGN.md §8f */
-            error_log(X, 62);
-            return 3;
+            double st_in[4] = {st[0], st[1], st[2], st[3]};
+            lambertian(X, rng, pos, st, dir);
+            peel_surface(X, pos, st_in, cell, face);
+            cell[0] = cell[0] + 1;
         }
         tau_run += tau_cell;
     }
@@ -774,7 +1031,16 @@ static int transport_packet(ctx* X, uint64_t seed, uint64_t id, double* nscat_ou
     X->cnt[ARTES_CNT_PACKETS]++;
     X->peel_sum = 0.0;
     *nscat_out = 0.0;
-    emit_star(X, &rng, pos, dir, face, cell);
+    const int planet = (p->photon_source == 2);
+    if (planet) {                                  /* ARTES.f90:599-622 */
+        double bias_weight;
+        emit_planet(X, &rng, pos, dir, face, cell, &bias_weight);
+        st[0] = st[0] * bias_weight / X->th_weight[cidx(X->g, cell)];
+        X->totals[8] += st[0];
+        if (peel_thermal(X, pos, st, cell, face)) { error_log(X, 47); X->cnt[ARTES_CNT_DROPPED]++; return 3; }
+    } else {
+        emit_star(X, &rng, pos, dir, face, cell);
+    }
 
     /* optical depth to the boundary or the surface (ARTES.f90:625-656) */
     double tau_first = 0.0, xc = pos[0], yc = pos[1], zc = pos[2], fd;
@@ -800,6 +1066,7 @@ static int transport_packet(ctx* X, uint64_t seed, uint64_t id, double* nscat_ou
         } else tau = -log(1.0 - xi);
     }
     int r = propagate(X, &rng, pos, dir, face, cell, tau, st);
+    if (r == 1 && planet) X->totals[9] += st[0];   /* flux_exit, ARTES.f90:780 */
     if (r == 1) { X->cnt[ARTES_CNT_EXITED]++; return 1; }
     if (r == 2) { X->cnt[ARTES_CNT_ABSORBED]++; return 2; }
     if (r == 3) { X->cnt[ARTES_CNT_DROPPED]++; return 3; }
@@ -832,19 +1099,34 @@ static int transport_packet(ctx* X, uint64_t seed, uint64_t id, double* nscat_ou
         xi = rng_uniform(&rng);
         tau = -log(1.0 - xi);
         r = propagate(X, &rng, pos, dir, face, cell, tau, st);
+        if (r == 1 && planet) X->totals[9] += st[0];   /* flux_exit, ARTES.f90:953 */
         if (r == 1) { X->cnt[ARTES_CNT_EXITED]++; return 1; }
         if (r == 2) { X->cnt[ARTES_CNT_ABSORBED]++; return 2; }
         if (r == 3) { error_log(X, 5); X->cnt[ARTES_CNT_DROPPED]++; return 3; }
     }
 }
 
-/* Run packets [first, first+n). detector [4][4][ny][nx], totals[8], counters, err are ACCUMULATED into.
+/* Run packets [first, first+n). detector [4][4][ny][nx], totals[ARTES_NUM_TOTALS], counters, err are ACCUMULATED into.
  * records (optional) [n][4] = {peeled I sum, scatters, crossings, end state}. */
 int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
                int nthreads, double* detector, double* totals, uint64_t* counters, uint64_t* err, double* records) {
     if (!g || !p || !detector) return -22;
-    if (p->photon_source != 1) return -38;
-    int cell_depth = p->cell_depth >= 0 ? p->cell_depth : oracle_cell_depth(g, p->wl_index);
+    if (p->photon_source != 1 && p->photon_source != 2) return -22;
+    double* th_cdf = NULL;
+    double* th_weight = NULL;
+    double th_total = 0.0;
+    int cell_depth, th_cd0 = 0;
+    if (p->photon_source == 2) {
+        th_cdf = (double*)malloc(sizeof(double) * (size_t)g->ncell);
+        th_weight = (double*)malloc(sizeof(double) * (size_t)g->ncell);
+        int rc = (th_cdf && th_weight) ? oracle_thermal(g, p->wl_index, p->thermal_weight, p->ring, &cell_depth, &th_total,
+                                                         NULL, th_weight, th_cdf) : -12;
+        if (rc) { free(th_cdf); free(th_weight); return rc; }
+        th_cd0 = cell_depth;
+        if (p->cell_depth >= 0) cell_depth = p->cell_depth;
+    } else {
+        cell_depth = p->cell_depth >= 0 ? p->cell_depth : oracle_cell_depth(g, p->wl_index);
+    }
     size_t detn = (size_t)16 * p->nx * p->ny;
 #ifdef _OPENMP
     if (nthreads <= 0) nthreads = omp_get_max_threads();
@@ -854,8 +1136,8 @@ int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, 
     double* dets = (double*)calloc(detn * (size_t)nthreads, sizeof(double));
     uint64_t* cnts = (uint64_t*)calloc((size_t)ARTES_NUM_COUNTERS * nthreads, sizeof(uint64_t));
     uint64_t* errs = (uint64_t*)calloc((size_t)ARTES_NUM_ERR * nthreads, sizeof(uint64_t));
-    double* tots = (double*)calloc((size_t)8 * nthreads, sizeof(double));
-    if (!dets || !cnts || !errs || !tots) { free(dets); free(cnts); free(errs); free(tots); return -12; }
+    double* tots = (double*)calloc((size_t)ARTES_NUM_TOTALS * nthreads, sizeof(double));
+    if (!dets || !cnts || !errs || !tots) { free(dets); free(cnts); free(errs); free(tots); free(th_cdf); free(th_weight); return -12; }
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads)
 #endif
@@ -875,8 +1157,9 @@ int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, 
         X.detector = dets + detn * t;
         X.cnt = cnts + (size_t)ARTES_NUM_COUNTERS * t;
         X.err = errs + (size_t)ARTES_NUM_ERR * t;
-        X.totals = tots + (size_t)8 * t;
+        X.totals = tots + (size_t)ARTES_NUM_TOTALS * t;
         X.cur_pix = -1;
+        X.th_cdf = th_cdf; X.th_weight = th_weight; X.th_total = th_total; X.th_cd0 = th_cd0;
 #ifdef _OPENMP
 #pragma omp for schedule(static)
 #endif
@@ -898,9 +1181,9 @@ int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, 
         for (size_t i = 0; i < detn; i++) detector[i] += dets[detn * t + i];
         if (counters) for (int i = 0; i < ARTES_NUM_COUNTERS; i++) counters[i] += cnts[(size_t)ARTES_NUM_COUNTERS * t + i];
         if (err) for (int i = 0; i < ARTES_NUM_ERR; i++) err[i] += errs[(size_t)ARTES_NUM_ERR * t + i];
-        if (totals) for (int i = 0; i < 8; i++) totals[i] += tots[(size_t)8 * t + i];
+        if (totals) for (int i = 0; i < ARTES_NUM_TOTALS; i++) totals[i] += tots[(size_t)ARTES_NUM_TOTALS * t + i];
     }
-    free(dets); free(cnts); free(errs); free(tots);
+    free(dets); free(cnts); free(errs); free(tots); free(th_cdf); free(th_weight);
     return 0;
 }
 

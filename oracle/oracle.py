@@ -11,7 +11,7 @@ import subprocess
 
 import numpy as np
 
-from artes_amd.abi import ARTES_NUM_COUNTERS, ARTES_NUM_ERR, GridArrays, GridDesc, RunParams
+from artes_amd.abi import ARTES_NUM_COUNTERS, ARTES_NUM_ERR, ARTES_NUM_TOTALS, GridArrays, GridDesc, RunParams
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liboracle.so")
@@ -39,6 +39,9 @@ def lib():
                                  C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
         L.oracle_max_threads.restype = C.c_int
+        dp = C.POINTER(C.c_double)
+        L.oracle_thermal.restype = C.c_int
+        L.oracle_thermal.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), dp, dp, dp, dp]
         _lib = L
     return _lib
 
@@ -53,9 +56,22 @@ class OracleGrid:
     def cell_depth(self, wl: int = 0) -> int:
         return lib().oracle_cell_depth(self.h, wl)
 
+    def thermal(self, wl: int = 0, thermal_weight: bool = True, ring: bool = False):
+        """grid_initialize(2), planet branch: (cell_depth, emissivity_total, cell_luminosity[nphi][ntheta][nr])."""
+        cd = C.c_int()
+        tot = C.c_double()
+        a = self.arrays
+        lum = np.zeros((a.nphi, a.ntheta, a.nr))
+        dp = C.POINTER(C.c_double)
+        rc = lib().oracle_thermal(self.h, wl, int(bool(thermal_weight)), int(bool(ring)), C.byref(cd), C.byref(tot),
+                                  lum.ctypes.data_as(dp), None, None)
+        if rc != 0:
+            raise RuntimeError(f"oracle_thermal failed: {rc}")
+        return cd.value, tot.value, lum
+
     def run(self, params: RunParams, first: int, n: int, seed: int, threads: int = 0, records: bool = False):
         det = np.zeros((4, 4, params.ny, params.nx))
-        tot = np.zeros(8)
+        tot = np.zeros(ARTES_NUM_TOTALS)
         cnt = np.zeros(ARTES_NUM_COUNTERS, dtype=np.uint64)
         err = np.zeros(ARTES_NUM_ERR, dtype=np.uint64)
         rec = np.zeros((n, 4)) if records else None

@@ -21,7 +21,7 @@ def declared_functions():
 def test_header_declares_the_boundary():
     names = declared_functions()
     for required in ("artes_grid_create", "artes_grid_destroy", "artes_run", "artes_run_device",
-                     "artes_run_trace", "artes_last_kernel_ms", "artes_abi_version"):
+                     "artes_run_trace", "artes_last_kernel_ms", "artes_abi_version", "artes_grid_thermal"):
         assert required in names
 
 
@@ -31,7 +31,7 @@ def test_library_exports_every_symbol():
     lib = engine.lib()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.artes_abi_version() == 1
+    assert lib.artes_abi_version() == 2
     assert b"gfx950" in lib.artes_build_info()
 
 
@@ -43,12 +43,32 @@ def test_library_is_gfx950_code_object():
     assert b"amdgcn-amd-amdhsa--gfx950" in blob          # offload bundle entry for gfx950
 
 
-def test_struct_layouts_match_header():
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirror (artes_amd/abi.py) has the C compiler's sizes and offsets."""
+    import shutil
+    import subprocess
+
     from artes_amd.abi import GridDesc, RunParams
 
-    # 4 int32 + 8 pointers + 1 double ; 8 int32 + 9 doubles
-    assert ctypes.sizeof(GridDesc) == 16 + 8 * 8 + 8
-    assert ctypes.sizeof(RunParams) == 32 + 9 * 8
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    lines = []
+    for cls, cname in ((GridDesc, "artes_grid_desc"), (RunParams, "artes_run_params")):
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "artes_amd.h"\nint main(void){' + "".join(lines)
+                   + "return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for cls, cname in ((GridDesc, "artes_grid_desc"), (RunParams, "artes_run_params")):
+        assert got[(cname, "size")] == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)
 
 
 def test_product_path_does_not_import_oracle():
