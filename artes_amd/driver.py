@@ -99,10 +99,14 @@ def planck(temperature: float, wavelength_m: float, photon_source: int) -> float
     return (2.0 * HH * CC * CC / (wavelength_m ** 5.0)) / math.expm1(x) if x < 700 else 0.0
 
 
-def package_energy(cfg: RunConfig, wavelength_m: float, r_top: float, packages: int, det_phi: float) -> float:
-    """``photon_package`` star branch (``ARTES.f90:2515-2531``)."""
-    if cfg.photon_source != 1:
-        raise NotImplementedError("photon:source=planet is not implemented yet (DESIGN.md, next rows)")
+def package_energy(cfg: RunConfig, wavelength_m: float, r_top: float, packages: int, det_phi: float,
+                   emissivity_total: float | None = None) -> float:
+    """``photon_package`` (``ARTES.f90:2509-2539``).  The planet source needs the total weighted
+    emissivity of the wavelength (``Grid.thermal``)."""
+    if cfg.photon_source == 2:
+        if emissivity_total is None:
+            raise ValueError("photon:source=planet: package_energy needs the emissivity total")
+        return emissivity_total / (cfg.distance_planet * cfg.distance_planet * float(packages))
     flux = planck(cfg.t_star, wavelength_m, 1)
     e = PI * flux * r_top * r_top * cfg.r_star * cfg.r_star / (
         cfg.orbit * cfg.orbit * cfg.distance_planet * cfg.distance_planet * float(packages))
@@ -203,6 +207,22 @@ def write_normalization(outdir: str, cfg: RunConfig, wavelength_m: float, r_top:
     n2 = 1.0e-6 * flux * r_top ** 2 * cfg.r_star ** 2 / (cfg.orbit ** 2 * cfg.distance_planet ** 2)
     _append(os.path.join(outdir, "normalization.dat"), None,
             " " + " ".join(_fmt(v) for v in (wavelength_m * 1e6, n1, n2)) + "\n")
+
+
+def write_luminosity(outdir: str, wavelength_m: float, flux_emitted: float, flux_exit: float, e_pack: float) -> None:
+    """``luminosity.dat`` of the planet source (``ARTES.f90:3660-3680``): wavelength [m] (the
+    reference's header says [deg]), emitted and emergent luminosity [W micron-1], and the
+    emergent sum of packet weights."""
+    _append(os.path.join(outdir, "luminosity.dat"),
+            " # Wavelength [deg] - Emitted luminosity [W micron-1] - Emergent luminosity [W micron-1] - "
+            "Emergent luminosity [a.u.]\n\n",
+            " " + " ".join(_fmt(v) for v in (wavelength_m, flux_emitted * e_pack * 1.0e-6,
+                                             flux_exit * e_pack * 1.0e-6, flux_exit)) + "\n")
+
+
+def write_cell_luminosity(outdir: str, lum: np.ndarray) -> None:
+    """``cell_luminosity.fits`` (``write_fits_3D``, ``ARTES.f90:3658``): [nphi][ntheta][nr] in C order."""
+    fitsio.write(os.path.join(outdir, "cell_luminosity.fits"), np.asarray(lum, dtype=np.float64))
 
 
 def write_cell_depth(outdir: str, wavelength_m: float, cell_depth: int) -> None:

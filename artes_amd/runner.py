@@ -44,6 +44,9 @@ class Transport:
     def cell_depth(self, wl: int) -> int:
         return self.grid.cell_depth(wl)
 
+    def thermal(self, wl: int, thermal_weight: bool, ring: bool):
+        return self.grid.thermal(wl, thermal_weight, ring)
+
     def run(self, params, first: int, n: int, seed: int):
         return self.grid.run(params, first, n, seed)
 
@@ -139,39 +142,59 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
     err_total = np.zeros(64, dtype=np.uint64)
     call = [0]
 
+    planet = cfg.photon_source == 2
+    thermal = {}
+
+    def source(wl: int):
+        """(cell_depth, emissivity_total, cell_luminosity) of the wavelength: grid_initialize(2)."""
+        if wl not in thermal:
+            thermal[wl] = (transport.thermal(wl, cfg.thermal_weight, cfg.ring) if planet
+                           else (transport.cell_depth(wl), None, None))
+        return thermal[wl]
+
+    def energy(wl: int, det_phi: float) -> float:
+        return driver.package_energy(cfg, wavelengths[wl], r_top, packages, det_phi, emissivity_total=source(wl)[1])
+
+    def write_source(wl: int, res, mono: bool):
+        """normalization.dat (star) or luminosity.dat / cell_luminosity.fits (planet), ARTES.f90:3623-3685."""
+        if planet:
+            if mono:
+                driver.write_cell_luminosity(out_dir, source(wl)[2])
+            e_pack = source(wl)[1] / float(packages)
+            driver.write_luminosity(out_dir, wavelengths[wl], float(res.totals[8]), float(res.totals[9]), e_pack)
+        else:
+            driver.write_normalization(out_dir, cfg, wavelengths[wl], r_top)
+
     def transport_call(wl: int, det_phi: float):
-        params = driver.run_params(cfg, det, wl, det_phi=det_phi, cell_depth=transport.cell_depth(wl))
+        params = driver.run_params(cfg, det, wl, det_phi=det_phi, cell_depth=source(wl)[0])
         base = call[0] * packages
         call[0] += 1
         res = dist.run_sharded(lambda first, n, s: transport.run(params, base + first, n, s), packages, seed, r)
         return res
 
     mode = cfg.mode
-    if cfg.photon_source != 1:
-        print("photon:source=planet is not implemented yet (DESIGN.md, next rows)", file=stdout)
-        return 0
     if mode == "imaging_mono":
         wl = 0
         res = transport_call(wl, det.det_phi)
         err_total += res.err
         if r.rank == 0:
-            E = driver.package_energy(cfg, wavelengths[wl], r_top, packages, det.det_phi)
+            E = energy(wl, det.det_phi)
             d = driver.scale_detector(res.det[:3], E)
             ph = driver.photometry(d)
             driver.write_stokes_outputs(out_dir, d, det.pixel_scale)
             driver.write_photometry(out_dir, wavelengths[wl], ph)
-            driver.write_normalization(out_dir, cfg, wavelengths[wl], r_top)
-            driver.write_cell_depth(out_dir, wavelengths[wl], transport.cell_depth(wl))
+            write_source(wl, res, True)
+            driver.write_cell_depth(out_dir, wavelengths[wl], source(wl)[0])
     elif mode == "spectrum":                              # ARTES.f90:132-166
         for wl in range(wavelengths.size):
             res = transport_call(wl, det.det_phi)
             err_total += res.err
             if r.rank == 0:
-                E = driver.package_energy(cfg, wavelengths[wl], r_top, packages, det.det_phi)
+                E = energy(wl, det.det_phi)
                 d = driver.scale_detector(res.det[:3], E)
                 driver.write_spectrum_line(out_dir, wavelengths[wl], d)
-                driver.write_normalization(out_dir, cfg, wavelengths[wl], r_top)
-                driver.write_cell_depth(out_dir, wavelengths[wl], transport.cell_depth(wl))
+                write_source(wl, res, False)
+                driver.write_cell_depth(out_dir, wavelengths[wl], source(wl)[0])
     elif mode == "imaging_broad":                         # ARTES.f90:168-204
         acc = None
         E = 0.0
@@ -181,7 +204,9 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
             acc = res.det[:3].copy() if acc is None else acc + res.det[:3]
             # every call rescales the running thread sums by the CURRENT wavelength's
             # package energy (ARTES.f90:959-975 inside the loop): the last one wins
-            E = driver.package_energy(cfg, wavelengths[wl], r_top, packages, det.det_phi)
+            E = energy(wl, det.det_phi)
+            if r.rank == 0 and planet:
+                write_source(wl, res, False)
         if r.rank == 0:
             d = driver.scale_detector(acc, E)
             driver.write_stokes_outputs(out_dir, d, det.pixel_scale)
@@ -191,11 +216,11 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
             res = transport_call(wl, phi)
             err_total += res.err
             if r.rank == 0:
-                E = driver.package_energy(cfg, wavelengths[wl], r_top, packages, phi)
+                E = energy(wl, phi)
                 d = driver.scale_detector(res.det[:3], E)
                 driver.write_phase_line(out_dir, phi, d)
-                if phi < PI / 180.0:
-                    driver.write_normalization(out_dir, cfg, wavelengths[wl], r_top)
+                if planet or phi < PI / 180.0:
+                    write_source(wl, res, False)
     else:
         print("No detector type (detector:type) selected", file=stdout)
         return 0

@@ -46,6 +46,9 @@ class OracleTransport:
     def cell_depth(self, wl):
         return self.g.cell_depth(wl)
 
+    def thermal(self, wl, thermal_weight, ring):
+        return self.g.thermal(wl, thermal_weight, ring)
+
     def run(self, params, first, n, seed):
         d, t, c, e, _ = self.g.run(params, first, n, seed, threads=4)
         return RunResult(d, t, c, e)
@@ -83,6 +86,53 @@ def test_spectrum_and_phase_modes(tmp_path):
     assert runner.run(["atm", "2e3", "-o", "ph", "--seed", "1"], root=str(tmp_path), transport_factory=OracleTransport) == 0
     rows = [l for l in (tmp_path / "output/ph/output/phase.dat").read_text().splitlines() if l.strip() and "#" not in l]
     assert len(rows) == 73 and float(rows[0].split()[0]) == 0.0 and float(rows[-1].split()[0]) == 180.0
+
+
+def _make_thermal_input(root, mode="imaging_mono"):
+    d = root / "input" / "hot"
+    d.mkdir(parents=True)
+    (d / "artes.in").write_text(ARTES_IN.replace("photon:source=star", "photon:source=planet").format(mode=mode))
+    atm = synthetic.make_thermal(nr=8, ntheta=4, nphi=4, tau_abs=2.0, tau_sca=1.0,
+                                 temperature=lambda rc: 1100.0 - 3e-3 * (rc - rc[0]), wavelength=(5.0, 10.0))
+    atmosphere.write_atmosphere_fits(str(d / "atmosphere.fits"), atm)
+    return atm
+
+
+def _luminosity_rows(path):
+    return [[float(x) for x in l.split()] for l in open(path).read().splitlines() if l.strip() and "#" not in l]
+
+
+def test_planet_source_outputs_cpu_plumbing(tmp_path):
+    """photon:source=planet: luminosity.dat (emitted luminosity = sum of the cell luminosities
+    within the Monte-Carlo error), cell_luminosity.fits, thermal cell_depth.dat."""
+    from oracle.oracle import OracleGrid
+
+    atm = _make_thermal_input(tmp_path)
+    n = 40000
+    assert runner.run(["hot", str(n), "-o", "th", "--seed", "2"], root=str(tmp_path), transport_factory=OracleTransport) == 0
+    out = tmp_path / "output" / "th" / "output"
+    for f in ("stokes.fits", "error.fits", "photometry.dat", "luminosity.dat", "cell_luminosity.fits", "cell_depth.dat"):
+        assert (out / f).exists(), f
+    assert not (out / "normalization.dat").exists()
+    cd, total, lum = OracleGrid(atm).thermal(0, True, False)
+    rows = _luminosity_rows(out / "luminosity.dat")
+    assert len(rows) == 1 and rows[0][0] == pytest.approx(5.0e-6)
+    assert rows[0][1] == pytest.approx(lum.sum() * 1e-6, rel=0.02)          # emitted [W micron-1]
+    assert 0.0 < rows[0][2] < rows[0][1]                                     # emergent < emitted
+    np.testing.assert_allclose(fitsio.read(out / "cell_luminosity.fits")[0].data, lum, rtol=1e-12)
+    assert int(open(out / "cell_depth.dat").read().split()[-1]) == cd
+    s = fitsio.read(out / "stokes.fits")[0].data
+    assert s[0].sum() > 0
+
+
+@pytest.mark.gpu
+def test_planet_source_cli_on_gpu(tmp_path, require_gpu):
+    _make_thermal_input(tmp_path, mode="spectrum")
+    assert runner.run(["hot", "2e5", "-o", "ths", "--seed", "4"], root=str(tmp_path)) == 0
+    rows = _luminosity_rows(tmp_path / "output/ths/output/luminosity.dat")
+    assert len(rows) == 2 and all(0.0 < r[2] < r[1] for r in rows)
+    spec = [l for l in (tmp_path / "output/ths/output/spectrum.dat").read_text().splitlines() if l.strip() and "#" not in l]
+    assert len(spec) == 2 and all(float(l.split()[1]) > 0 for l in spec)
 
 
 @pytest.mark.gpu
