@@ -9,8 +9,8 @@
 // Along a straight trace the faces of a coordinate family do not change until the trace
 // crosses a face of THAT family: crossing a phi face leaves the cell's radial shell and
 // theta band, so their candidate crossings are still the ones found before.  This
-// kernel therefore keeps the six candidates (as trace parameters t) in registers and,
-// after each crossing, re-evaluates only the family that was crossed -- with the
+// kernel therefore keeps, per family, the nearest face ahead (as a trace parameter t) in
+// registers and, after each crossing, re-evaluates only the family that was crossed -- with the
 // reference's own formulas, tolerances and same-face rules, from the current position.
 // That is one pair of quadratics (spheres or cones) or one pair of plane intersections
 // per step instead of four quadratics and three plane intersections.  The family to
@@ -30,10 +30,11 @@
 namespace artes {
 
 // ------------------------------------------------------------ fast math ---
-// a / b to ~1 ulp for normal operands (b = 0 gives inf/nan: callers select it away)
+// a / b to ~1 ulp for normal operands (b = 0 gives inf/nan: callers select it away).
+// v_rcp_f64 is good to ~2^-23; one Newton step squares that error, and the residual
+// correction of the quotient squares it again, below the rounding of the result.
 __device__ __forceinline__ double fast_div(double a, double b) {
     double r = __builtin_amdgcn_rcp(b);
-    r = fma(fma(-b, r, 1.0), r, r);
     r = fma(fma(-b, r, 1.0), r, r);
     const double q = a * r;
     return fma(fma(-b, q, a), r, q);
@@ -205,8 +206,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     Rng rng{0, 0};
     int tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0, pending = 0;
     double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, tpar = 0, inz = 0;
-    // cached candidates as trace parameters: rin, tin, pin, rout, tout, pout
-    double c0 = NONE, c1 = NONE, c2 = NONE, c3 = NONE, c4 = NONE, c5 = NONE;
+    // per family (radial, theta, phi) the nearest face ahead as a trace parameter, and its
+    // side (bit f of `sides`: 0 inner, 1 outer face)
+    double m0 = NONE, m1 = NONE, m2 = NONE;
+    int sides = 0;
     uint32_t c_cross = 0, c_peel = 0;
 
     // a trace starts at the packet position with zero optical depth
@@ -264,37 +267,47 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             const int fam = G3D ? __builtin_ctz(pending) : 0;
             double din, dout;
             family_candidates<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, tft, tfi, tcr, tct, tcp, -tz * inz, din, dout);
-            const double tin = din > 0.0 ? tpar + din : NONE, tout = dout > 0.0 ? tpar + dout : NONE;
-            if (fam == 0) { c0 = tin; c3 = tout; }
+            // the evaluated family's nearest face ahead goes to the cache: the other face of a
+            // family only matters while the packet sits on the first (and then the family
+            // is evaluated again)
+            const bool uo = dout > 0.0 && !(din > 0.0 && din <= dout);
+            const double dm = uo ? dout : din;
+            const double tm = dm > 0.0 ? tpar + dm : NONE;
+            if (fam == 0) m0 = tm;
             if constexpr (G3D) {
-                if (fam == 1) { c1 = tin; c4 = tout; }
-                if (fam == 2) { c2 = tin; c5 = tout; }
+                if (fam == 1) m1 = tm;
+                if (fam == 2) m2 = tm;
             }
+            sides = (sides & ~(1 << fam)) | ((uo ? 1 : 0) << fam);
             pending &= pending - 1;
             if (pending == 0) {
                 // ------------------------------------------------ trace step
-                // distances: exact for the family just evaluated, from the cache otherwise
-                const double e0 = fam == 0 ? din : c0 - tpar, e3 = fam == 0 ? dout : c3 - tpar;
-                double e1 = 0.0, e2 = 0.0, e4 = 0.0, e5 = 0.0;
+                // candidates: both faces of the family just evaluated (exact distances) and
+                // the cached nearest face of each other family; `which` = family + 3 * side
+                double e0 = -1.0, e1 = -1.0, e2 = -1.0;
                 if constexpr (G3D) {
-                    e1 = fam == 1 ? din : c1 - tpar; e4 = fam == 1 ? dout : c4 - tpar;
-                    e2 = fam == 2 ? din : c2 - tpar; e5 = fam == 2 ? dout : c5 - tpar;
+                    e0 = fam == 0 ? -1.0 : m0 - tpar;
+                    e1 = fam == 1 ? -1.0 : m1 - tpar;
+                    e2 = fam == 2 ? -1.0 : m2 - tpar;
                 }
                 // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
                 double best = 1.e100;
                 int which = -1;
 #define ARTES_CONSIDER(dd, w, thr) if ((dd) > (thr) && (dd) < best) { best = (dd); which = (w); }
-                ARTES_CONSIDER(e0, 0, 1.e-9)
-                if constexpr (G3D) { ARTES_CONSIDER(e1, 1, 1.e-9) ARTES_CONSIDER(e2, 2, 1.e-9) }
-                ARTES_CONSIDER(e3, 3, 1.e-9)
-                if constexpr (G3D) { ARTES_CONSIDER(e4, 4, 1.e-9) ARTES_CONSIDER(e5, 5, 1.e-9) }
+#define ARTES_PASS(thr)                                                                    \
+                ARTES_CONSIDER(din, fam, thr)                                              \
+                ARTES_CONSIDER(dout, fam + 3, thr)                                         \
+                if constexpr (G3D) {                                                       \
+                    ARTES_CONSIDER(e0, 0 + 3 * (sides & 1), thr)                           \
+                    ARTES_CONSIDER(e1, 1 + 3 * ((sides >> 1) & 1), thr)                    \
+                    ARTES_CONSIDER(e2, 2 + 3 * ((sides >> 2) & 1), thr)                    \
+                }
+                ARTES_PASS(1.e-9)
                 if (which < 0) {
                     best = 1.e100;
-                    ARTES_CONSIDER(e0, 0, 1.e-12)
-                    if constexpr (G3D) { ARTES_CONSIDER(e1, 1, 1.e-12) ARTES_CONSIDER(e2, 2, 1.e-12) }
-                    ARTES_CONSIDER(e3, 3, 1.e-12)
-                    if constexpr (G3D) { ARTES_CONSIDER(e4, 4, 1.e-12) ARTES_CONSIDER(e5, 5, 1.e-12) }
+                    ARTES_PASS(1.e-12)
                 }
+#undef ARTES_PASS
 #undef ARTES_CONSIDER
                 // next_cell (ARTES.f90:2671-2798)
                 int nft = 0, nfi = -999, ncr = tcr, nct = tct, ncp = tcp;
