@@ -60,6 +60,8 @@ struct DevRun {
     unsigned long long* __restrict__ cnt;   // [ARTES_NUM_COUNTERS]
     unsigned long long* __restrict__ err;   // [ARTES_NUM_ERR]
     double* __restrict__ rec;       // [n][4] (TRACE builds)
+    double* __restrict__ flow_g;    // [ncell][3] flow_global accumulators, or null
+    double* __restrict__ flow_t;    // [ncell][4] flow_latitudinal accumulators, or null
 };
 
 // ------------------------------------------------------------------- RNG ---

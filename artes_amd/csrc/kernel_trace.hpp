@@ -177,6 +177,28 @@ __device__ __forceinline__ void family_candidates(const DevGrid& G, const TraceT
     d_out = isP ? p_out : (isT ? t_out : r_out);
 }
 
+// Energy-transport diagnostics of a propagation segment (output:flow_global /
+// output:flow_latitudinal).  add_flow_global (ARTES.f90:4992-5011): the direction's
+// (r, theta, phi) components at the segment's end point, times segment length and
+// Stokes I; add_flow (5013-5045): Stokes I through the cell's upper (lat 0) or lower
+// (1) radial face, or its southern (2) or northern (3) theta face (lat -1: none).
+__device__ __noinline__ void flow_segment(double* flow_g, double* flow_t, int cell, double x, double y, double z,
+                                          double nx, double ny, double nz, double len, double w, int lat) {
+    if (flow_g) {
+        const double th = acos(z / sqrt(x * x + y * y + z * z));
+        const double ph = atan2(y, x);
+        const double st = sin(th), ct = cos(th), sp = sin(ph), cp = cos(ph);
+        const double rd = st * cp * nx + st * sp * ny + ct * nz;
+        const double td = ct * cp * nx + ct * sp * ny - st * nz;
+        const double pd = -sp * nx + cp * ny;
+        double* f = flow_g + 3 * (size_t)cell;
+        atomicAdd(f + 0, rd * len * w);
+        atomicAdd(f + 1, td * len * w);
+        atomicAdd(f + 2, pd * len * w);
+    }
+    if (flow_t && lat >= 0) atomicAdd(flow_t + 4 * (size_t)cell + lat, w);
+}
+
 // -------------------------------------------------------------- k_trace ---
 // A lane takes a slot from the trace list and runs its traces back to back as long as
 // they chain inside the reference's packet loop: first optical depth -> propagation
@@ -184,7 +206,9 @@ __device__ __forceinline__ void family_candidates(const DevGrid& G, const TraceT
 // 788-813) -> k_event.  Everything a chain needs is loaded once at refill and kept in
 // registers (position, direction, RNG state, Stokes I); the slot is written back once
 // when the chain ends, so no transition waits on memory.
-template <bool G3D, bool OBL, int WPE>
+//
+// FLOW instantiations add the energy-transport diagnostics to propagation segments.
+template <bool G3D, bool OBL, int WPE, bool FLOW = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G, DevRun R, Pool S, Lists L) {
     extern __shared__ double s_tab[];
     const TraceTabs T = stage_trace_tables(G, s_tab);
@@ -331,6 +355,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 const bool prop = (mode == S_PROP);
                 const bool hit = prop && tacc + tau_cell > ttgt;
                 const bool stop = err || exit || surf || hit;
+                if constexpr (FLOW) {
+                    if (prop && !err && !hit) {   // the segment to the face (ARTES.f90:728-743, 889-904)
+                        const int lat = which == 3 ? 0 : which == 0 ? 1 : which == 4 ? 2 : which == 1 ? 3 : -1;
+                        flow_segment(R.flow_g, R.flow_t, cell, tx + best * nx, ty + best * ny, tz + best * nz, nx, ny, nz, best, wI, lat);
+                    }
+                }
                 if (!stop) {
                     tacc += tau_cell;
                     tx += best * nx; ty += best * ny; tz += best * nz;
@@ -344,6 +374,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     px = tx + s * nx; py = ty + s * ny; pz = tz + s * nz;
                     pcell = pack_cell(tcr, tct, tcp);
                     pface = 0;
+                    if constexpr (FLOW) flow_segment(R.flow_g, R.flow_t, cell, px, py, pz, nx, ny, nz, s, wI, -1);   // (715, 874)
                     const double xi = rng.uni();   // a killed packet's RNG state is not used again
                     bool kill = !R.photon_scattering || xi < R.fstop;
                     if (alb < 1.0 && alb > 0.0) wI *= alb / (1.0 - R.fstop);

@@ -84,6 +84,7 @@ struct artes_grid {
     unsigned long long* d_err = nullptr;
     double* d_rec = nullptr;
     size_t rec_cap = 0;
+    double* d_flow = nullptr;         // scratch flow accumulators of the host-pointer variant [7][ncell]
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     int max_blocks = 0;
@@ -168,7 +169,8 @@ void artes_grid_destroy(artes_grid* g) {
     hipSetDevice(g->device);
     void* ptrs[] = {g->d_rf2, g->d_thetaf, g->d_tan2, g->d_phif, g->d_phis, g->d_phic, g->d_kappa, g->d_albedo,
                     g->d_mats, g->d_cums, g->d_sc2, g->d_ss2, g->d_tplane, g->d_matid, g->d_copies, g->d_out,
-                    g->d_tot, g->d_cnt, g->d_err, g->d_rec, g->d_rfront, g->d_tcos, g->d_th_cdf, g->d_th_weight};
+                    g->d_tot, g->d_cnt, g->d_err, g->d_rec, g->d_rfront, g->d_tcos, g->d_th_cdf, g->d_th_weight,
+                    g->d_flow};
     for (void* p : ptrs)
         if (p) hipFree(p);
     void* eptrs[] = {g->pool_mem, g->d_lists[0], g->d_lists[1], g->d_event, g->d_emit, g->d_counts, g->d_grab, g->d_next};
@@ -278,16 +280,16 @@ static int32_t ensure_pool(artes_grid* g) {
 }
 
 // k_trace (kernel_trace.hpp) with its face tables in LDS
-template <bool G3D, bool OBL, int WPE>
+template <bool G3D, bool OBL, int WPE, bool FLOW = false>
 static void launch_trace(artes_grid* g, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
     const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
     int per_cu = 0;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, OBL, WPE>, BLOCK, lds);
+    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, OBL, WPE, FLOW>, BLOCK, lds);
     const char* bp = getenv("ARTES_TRACE_BPC");   // blocks per CU override (tuning)
     if (bp) per_cu = atoi(bp);
     g->trace_blocks = std::max(1, per_cu) * g->num_cus;
     timed(g, ARTES_K_TRACE, stream, [&] {
-        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
 }
 
@@ -296,7 +298,10 @@ static void launch_trace(artes_grid* g, const DevGrid& G, const DevRun& R, const
 template <bool G3D>
 static void launch_trace_any(artes_grid* g, int wpe, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
     const bool oblate = !(G.ax2 == 1.0 && G.by2 == 1.0 && G.cz2 == 1.0 && G.a == 1.0 && G.b == 1.0);
-    if (oblate) {
+    if (R.flow_g || R.flow_t) {   // diagnostics: one occupancy target only
+        if (oblate) launch_trace<G3D, true, 4, true>(g, G, R, L, stream);
+        else launch_trace<G3D, false, 4, true>(g, G, R, L, stream);
+    } else if (oblate) {
         if (wpe == 3) launch_trace<G3D, true, 3>(g, G, R, L, stream);
         else launch_trace<G3D, true, 4>(g, G, R, L, stream);
     } else {
@@ -398,12 +403,12 @@ extern "C" {
 
 static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
                       double* det_out, double* tot_out, unsigned long long* cnt_out, unsigned long long* err_out,
-                      double* rec, hipStream_t stream) {
+                      double* rec, hipStream_t stream, double* flow_g = nullptr, double* flow_t = nullptr) {
     const HostTables& T = g->T;
     if (!p) return fail(-22, "null params");
     if (p->photon_source != 1 && p->photon_source != 2) return fail(-22, "photon_source must be 1 (star) or 2 (planet)");
-    if (!use_event_engine() && (p->photon_source != 1 || p->surface_albedo > 0.0))
-        return fail(-38, "the persistent engine supports the star source without surface reflection only");
+    if (!use_event_engine() && (p->photon_source != 1 || p->surface_albedo > 0.0 || flow_g || flow_t))
+        return fail(-38, "the persistent engine supports the star source without surface reflection or flow output only");
     if (p->wl_index < 0 || p->wl_index >= T.nwav) return fail(-22, "wl_index out of range");
     if (p->nx < 1 || p->ny < 1 || (size_t)p->nx * p->ny > (1u << 26)) return fail(-22, "bad detector size");
     HIP_TRY(hipSetDevice(g->device));
@@ -476,6 +481,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.surface_albedo = p->surface_albedo; R.theta_star = p->theta_star; R.phi_star = p->phi_star;
     R.det = g->d_copies; R.det_stride = stride;
     R.tot2 = tot_out; R.cnt = cnt_out; R.err = err_out; R.rec = rec;
+    R.flow_g = flow_g; R.flow_t = flow_t;
 
     const bool g3d = (T.ntheta > 1 || T.nphi > 1);
     HIP_TRY(hipEventRecord(g->ev0, stream));
@@ -522,10 +528,33 @@ int32_t artes_run_device(artes_grid* g, const artes_run_params* p, uint64_t firs
                   nullptr, s);
 }
 
+int32_t artes_run_device_flow(artes_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
+                              double* det_dev, double* tot_dev, uint64_t* cnt_dev, uint64_t* err_dev,
+                              double* flow_global_dev, double* flow_latitudinal_dev, void* stream) {
+    if (!g || !det_dev) return fail(-22, "null argument");
+    HIP_TRY(hipSetDevice(g->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (!tot_dev) { HIP_TRY(hipMemsetAsync(g->d_tot, 0, 6 * sizeof(double), s)); }
+    if (!cnt_dev) { HIP_TRY(hipMemsetAsync(g->d_cnt, 0, ARTES_NUM_COUNTERS * 8, s)); }
+    if (!err_dev) { HIP_TRY(hipMemsetAsync(g->d_err, 0, ARTES_NUM_ERR * 8, s)); }
+    return launch(g, p, first, n, seed, det_dev, tot_dev ? tot_dev : g->d_tot,
+                  cnt_dev ? (unsigned long long*)cnt_dev : g->d_cnt, err_dev ? (unsigned long long*)err_dev : g->d_err,
+                  nullptr, s, flow_global_dev, flow_latitudinal_dev);
+}
+
 static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
-                        double* det, double* totals, uint64_t* counters, uint64_t* err, double* records) {
+                        double* det, double* totals, uint64_t* counters, uint64_t* err, double* records,
+                        double* flow_global = nullptr, double* flow_latitudinal = nullptr) {
     if (!g || !p) return fail(-22, "null argument");
     HIP_TRY(hipSetDevice(g->device));
+    const size_t nc = (size_t)g->T.ncell;
+    double *fg = nullptr, *ft = nullptr;
+    if (flow_global || flow_latitudinal) {
+        if (!g->d_flow) HIP_TRY(hipMalloc((void**)&g->d_flow, 7 * nc * sizeof(double)));
+        HIP_TRY(hipMemset(g->d_flow, 0, 7 * nc * sizeof(double)));
+        if (flow_global) fg = g->d_flow;
+        if (flow_latitudinal) ft = g->d_flow + 3 * nc;
+    }
     const size_t stride = (size_t)16 * p->nx * p->ny;
     if (g->out_cap < stride) {
         if (g->d_out) hipFree(g->d_out);
@@ -546,9 +575,15 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
     HIP_TRY(hipMemset(g->d_tot, 0, 6 * sizeof(double)));
     HIP_TRY(hipMemset(g->d_cnt, 0, ARTES_NUM_COUNTERS * 8));
     HIP_TRY(hipMemset(g->d_err, 0, ARTES_NUM_ERR * 8));
-    int32_t rc = launch(g, p, first, n, seed, g->d_out, g->d_tot, g->d_cnt, g->d_err, records ? g->d_rec : nullptr, 0);
+    int32_t rc = launch(g, p, first, n, seed, g->d_out, g->d_tot, g->d_cnt, g->d_err, records ? g->d_rec : nullptr, 0, fg, ft);
     if (rc) return rc;
     HIP_TRY(hipDeviceSynchronize());
+    if (fg || ft) {
+        std::vector<double> hf(7 * nc);
+        HIP_TRY(hipMemcpy(hf.data(), g->d_flow, hf.size() * sizeof(double), hipMemcpyDeviceToHost));
+        if (flow_global) for (size_t i = 0; i < 3 * nc; i++) flow_global[i] += hf[i];
+        if (flow_latitudinal) for (size_t i = 0; i < 4 * nc; i++) flow_latitudinal[i] += hf[3 * nc + i];
+    }
     std::vector<double> hd(stride);
     HIP_TRY(hipMemcpy(hd.data(), g->d_out, stride * sizeof(double), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < stride; i++) det[i] += hd[i];
@@ -583,6 +618,13 @@ int32_t artes_run(artes_grid* g, const artes_run_params* p, uint64_t first, uint
                   double* det, double* totals, uint64_t* counters, uint64_t* err) {
     if (!det) return fail(-22, "null detector");
     return run_host(g, p, first, n, seed, det, totals, counters, err, nullptr);
+}
+
+int32_t artes_run_flow(artes_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
+                       double* det, double* totals, uint64_t* counters, uint64_t* err, double* flow_global,
+                       double* flow_latitudinal) {
+    if (!det) return fail(-22, "null detector");
+    return run_host(g, p, first, n, seed, det, totals, counters, err, nullptr, flow_global, flow_latitudinal);
 }
 
 int32_t artes_run_trace(artes_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,

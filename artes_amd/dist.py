@@ -89,4 +89,7 @@ def run_sharded(transport, n_packets: int, seed: int, r: Rank):
         res.det, res.totals = det, tot
         res.counters = np.rint(cnt).astype(np.uint64)
         res.err = np.rint(err).astype(np.uint64)
+        for k in ("flow_global", "flow_latitudinal"):
+            if getattr(res, k, None) is not None:
+                setattr(res, k, allreduce_numpy([getattr(res, k)], r.world)[0])
     return res

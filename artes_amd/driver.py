@@ -225,6 +225,37 @@ def write_cell_luminosity(outdir: str, lum: np.ndarray) -> None:
     fitsio.write(os.path.join(outdir, "cell_luminosity.fits"), np.asarray(lum, dtype=np.float64))
 
 
+def flow_global_output(flow: np.ndarray, cell_depth: int) -> np.ndarray:
+    """``flow_global.fits`` contents (``write_output``, ``ARTES.f90:3715-3740``): per cell at
+    or above ``cell_depth`` the summed (r, theta, phi) transport vector normalised to unit
+    length (left as is when zero); cells below ``cell_depth`` are zero.  [nphi][ntheta][nr][3]."""
+    out = np.zeros_like(np.asarray(flow, dtype=np.float64))
+    f = np.asarray(flow, dtype=np.float64)[:, :, cell_depth:, :]
+    norm = np.sqrt(f[..., 0] ** 2 + f[..., 1] ** 2 + f[..., 2] ** 2)
+    out[:, :, cell_depth:, :] = np.where(norm[..., None] > 0.0, f / np.where(norm > 0.0, norm, 1.0)[..., None], f)
+    return out
+
+
+def flow_latitudinal_output(flow: np.ndarray, cell_depth: int, flux_exit: float | None) -> np.ndarray:
+    """``flow_latitudinal.fits`` contents (``ARTES.f90:3744-3766``): per cell at or above
+    ``cell_depth`` the Stokes I leaving upward, downward, southward and northward, divided
+    by the total emergent flux ``sum(flux_exit)``.  [nphi][ntheta][nr][4].  ``flux_exit``
+    None (star source, where the reference's array is undefined): not normalised."""
+    out = np.zeros_like(np.asarray(flow, dtype=np.float64))
+    out[:, :, cell_depth:, :] = np.asarray(flow, dtype=np.float64)[:, :, cell_depth:, :]
+    return out / flux_exit if flux_exit is not None else out
+
+
+def write_flow_global(outdir: str, flow: np.ndarray, cell_depth: int) -> None:
+    """``flow_global.fits`` (``write_fits_4D``, ``ARTES.f90:3738``)."""
+    fitsio.write(os.path.join(outdir, "flow_global.fits"), flow_global_output(flow, cell_depth))
+
+
+def write_flow_latitudinal(outdir: str, flow: np.ndarray, cell_depth: int, flux_exit: float | None) -> None:
+    """``flow_latitudinal.fits`` (``write_fits_4D``, ``ARTES.f90:3766``)."""
+    fitsio.write(os.path.join(outdir, "flow_latitudinal.fits"), flow_latitudinal_output(flow, cell_depth, flux_exit))
+
+
 def write_cell_depth(outdir: str, wavelength_m: float, cell_depth: int) -> None:
     """``cell_depth.dat`` (``ARTES.f90:3689-3711``)."""
     _append(os.path.join(outdir, "cell_depth.dat"), " # Wavelength [micron] - Cell depth\n\n",

@@ -66,6 +66,13 @@ def lib():
     L.artes_run_device.restype = C.c_int32
     L.artes_run_device.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.artes_run_flow.restype = C.c_int32
+    L.artes_run_flow.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64, dp, dp, up, up,
+                                 dp, dp]
+    L.artes_run_device_flow.restype = C.c_int32
+    L.artes_run_device_flow.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p]
     L.artes_run_trace.restype = C.c_int32
     L.artes_run_trace.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64, dp]
     L.artes_last_kernel_ms.restype = C.c_double
@@ -92,11 +99,13 @@ def _check(rc: int, what: str) -> None:
 class RunResult:
     """Raw (un-normalised) outputs of one transport call."""
 
-    def __init__(self, det, totals, counters, err):
+    def __init__(self, det, totals, counters, err, flow_global=None, flow_latitudinal=None):
         self.det = det            # [4][4][ny][nx]
         self.totals = totals      # [ARTES_NUM_TOTALS]
         self.counters = counters  # [ARTES_NUM_COUNTERS]
         self.err = err            # [ARTES_NUM_ERR]
+        self.flow_global = flow_global            # [nphi][ntheta][nr][3] or None
+        self.flow_latitudinal = flow_latitudinal  # [nphi][ntheta][nr][4] or None
 
     def counter(self, name: str) -> int:
         return int(self.counters[COUNTER_NAMES.index(name)])
@@ -106,6 +115,10 @@ class RunResult:
         self.totals += other.totals
         self.counters += other.counters
         self.err += other.err
+        for k in ("flow_global", "flow_latitudinal"):
+            a, b = getattr(self, k), getattr(other, k)
+            if b is not None:
+                setattr(self, k, b.copy() if a is None else a + b)
         return self
 
 
@@ -142,15 +155,27 @@ class Grid:
     def num_matrices(self) -> int:
         return lib().artes_grid_num_matrices(self.h)
 
-    def run(self, params: RunParams, first: int, n: int, seed: int) -> RunResult:
+    def run(self, params: RunParams, first: int, n: int, seed: int, flow_global: bool = False,
+            flow_latitudinal: bool = False) -> RunResult:
+        """One transport call; with ``flow_global`` / ``flow_latitudinal`` also the energy-transport
+        accumulators (``artes_run_flow``; output:flow_global / output:flow_latitudinal)."""
         det = np.zeros((4, 4, params.ny, params.nx))
         tot = np.zeros(ARTES_NUM_TOTALS)
         cnt = np.zeros(ARTES_NUM_COUNTERS, dtype=np.uint64)
         err = np.zeros(ARTES_NUM_ERR, dtype=np.uint64)
         dp, up = C.POINTER(C.c_double), C.POINTER(C.c_uint64)
-        _check(lib().artes_run(self.h, C.byref(params), int(first), int(n), int(seed), det.ctypes.data_as(dp),
-                               tot.ctypes.data_as(dp), cnt.ctypes.data_as(up), err.ctypes.data_as(up)), "artes_run")
-        return RunResult(det, tot, cnt, err)
+        if not (flow_global or flow_latitudinal):
+            _check(lib().artes_run(self.h, C.byref(params), int(first), int(n), int(seed), det.ctypes.data_as(dp),
+                                   tot.ctypes.data_as(dp), cnt.ctypes.data_as(up), err.ctypes.data_as(up)),
+                   "artes_run")
+            return RunResult(det, tot, cnt, err)
+        fg = np.zeros((self.nphi, self.ntheta, self.nr, 3)) if flow_global else None
+        ft = np.zeros((self.nphi, self.ntheta, self.nr, 4)) if flow_latitudinal else None
+        _check(lib().artes_run_flow(self.h, C.byref(params), int(first), int(n), int(seed), det.ctypes.data_as(dp),
+                                    tot.ctypes.data_as(dp), cnt.ctypes.data_as(up), err.ctypes.data_as(up),
+                                    fg.ctypes.data_as(dp) if fg is not None else None,
+                                    ft.ctypes.data_as(dp) if ft is not None else None), "artes_run_flow")
+        return RunResult(det, tot, cnt, err, fg, ft)
 
     def run_device(self, params: RunParams, first: int, n: int, seed: int, det_ptr: int, tot2_ptr: int = 0,
                    cnt_ptr: int = 0, err_ptr: int = 0, stream: int = 0) -> None:
@@ -158,6 +183,17 @@ class Grid:
         _check(lib().artes_run_device(self.h, C.byref(params), int(first), int(n), int(seed), C.c_void_p(det_ptr),
                                       C.c_void_p(tot2_ptr or None), C.c_void_p(cnt_ptr or None),
                                       C.c_void_p(err_ptr or None), C.c_void_p(stream or None)), "artes_run_device")
+
+    def run_device_flow(self, params: RunParams, first: int, n: int, seed: int, det_ptr: int, tot2_ptr: int = 0,
+                        cnt_ptr: int = 0, err_ptr: int = 0, flow_global_ptr: int = 0, flow_latitudinal_ptr: int = 0,
+                        stream: int = 0) -> None:
+        """``run_device`` plus device flow accumulators ([nphi][ntheta][nr][3] / [..][4] doubles)."""
+        _check(lib().artes_run_device_flow(self.h, C.byref(params), int(first), int(n), int(seed),
+                                           C.c_void_p(det_ptr), C.c_void_p(tot2_ptr or None),
+                                           C.c_void_p(cnt_ptr or None), C.c_void_p(err_ptr or None),
+                                           C.c_void_p(flow_global_ptr or None),
+                                           C.c_void_p(flow_latitudinal_ptr or None), C.c_void_p(stream or None)),
+               "artes_run_device_flow")
 
     def trace(self, params: RunParams, first: int, n: int, seed: int) -> np.ndarray:
         rec = np.zeros((n, 4))

@@ -9,7 +9,9 @@ the working directory must contain ``input/<atmosphere>/{artes.in,atmosphere.fit
 each ``-k`` is applied after ``artes.in`` and appended to the copied ``artes.in``.
 Outputs: ``output/<name>/{error.log,plot.dat}``, ``output/<name>/output/{stokes.fits,
 error.fits,photometry.dat,normalization.dat,cell_depth.dat}`` (imaging_mono), plus
-``spectrum.dat`` / ``phase.dat`` for the other modes.
+``spectrum.dat`` / ``phase.dat`` for the other modes, ``luminosity.dat`` /
+``cell_luminosity.fits`` for the planet source and ``flow_global.fits`` /
+``flow_latitudinal.fits`` with ``output:flow_global`` / ``output:flow_latitudinal``.
 
 The packet loop runs on the GPU engine (``artes_amd.engine``).  Under
 ``torchrun --nproc-per-node G`` every rank transports its shard on its own GPU and the
@@ -47,8 +49,8 @@ class Transport:
     def thermal(self, wl: int, thermal_weight: bool, ring: bool):
         return self.grid.thermal(wl, thermal_weight, ring)
 
-    def run(self, params, first: int, n: int, seed: int):
-        return self.grid.run(params, first, n, seed)
+    def run(self, params, first: int, n: int, seed: int, flow_global: bool = False, flow_latitudinal: bool = False):
+        return self.grid.run(params, first, n, seed, flow_global=flow_global, flow_latitudinal=flow_latitudinal)
 
 
 def _usage() -> None:
@@ -165,11 +167,25 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
         else:
             driver.write_normalization(out_dir, cfg, wavelengths[wl], r_top)
 
+    flows = {"flow_global": True} if cfg.flow_global else {}
+    if cfg.flow_theta:
+        flows["flow_latitudinal"] = True
+
     def transport_call(wl: int, det_phi: float):
         params = driver.run_params(cfg, det, wl, det_phi=det_phi, cell_depth=source(wl)[0])
         base = call[0] * packages
         call[0] += 1
-        res = dist.run_sharded(lambda first, n, s: transport.run(params, base + first, n, s), packages, seed, r)
+        res = dist.run_sharded(lambda first, n, s: transport.run(params, base + first, n, s, **flows), packages, seed, r)
+        if r.rank == 0 and flows:
+            # every write_output rewrites the flow files (ARTES.f90:3715-3768): the last call wins
+            if cfg.flow_global:
+                driver.write_flow_global(out_dir, res.flow_global, source(wl)[0])
+            if cfg.flow_theta:
+                if not planet:
+                    print("artes_amd: output:flow_latitudinal with photon:source=star -- the reference normalises "
+                          "by flux_exit, which only the planet source defines; written unnormalised", file=stdout)
+                driver.write_flow_latitudinal(out_dir, res.flow_latitudinal, source(wl)[0],
+                                              float(res.totals[9]) if planet else None)
         return res
 
     mode = cfg.mode

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define ARTES_ABI_VERSION 2
+#define ARTES_ABI_VERSION 3
 #define ARTES_NUM_TOTALS 10
 #define ARTES_NUM_ERR 64
 
@@ -157,6 +157,28 @@ int32_t artes_run_device(artes_grid* grid, const artes_run_params* params,
                          uint64_t first_packet, uint64_t n_packets, uint64_t seed,
                          double* detector_dev, double* totals_dev, uint64_t* counters_dev,
                          uint64_t* err_dev, void* stream);
+
+/* Energy-transport diagnostics (output:flow_global / output:flow_latitudinal): as
+ * artes_run / artes_run_device, plus per-cell accumulators in the reference's
+ * cell_flow_global / cell_flow layout with the component fastest (ARTES.f90:81-82,
+ * 2311-2322), ACCUMULATED into; either may be NULL (both NULL = plain run):
+ *   flow_global      [nphi][ntheta][nr][3]  sum over propagation segments of the
+ *                    direction's (r, theta, phi) component at the segment end x segment
+ *                    length x Stokes I (add_flow_global, 4992-5011)
+ *   flow_latitudinal [nphi][ntheta][nr][4]  Stokes I leaving the cell upward, downward,
+ *                    southward (theta increasing), northward (add_flow, 5013-5045)
+ * Only propagation segments count (peel-off and first-optical-depth traces do not:
+ * 715-743, 874-904).  The host writes flow_global.fits / flow_latitudinal.fits
+ * (write_output, 3715-3768).  The device variant takes device pointers. */
+int32_t artes_run_flow(artes_grid* grid, const artes_run_params* params,
+                       uint64_t first_packet, uint64_t n_packets, uint64_t seed,
+                       double* detector, double* totals, uint64_t* counters, uint64_t* err,
+                       double* flow_global, double* flow_latitudinal);
+int32_t artes_run_device_flow(artes_grid* grid, const artes_run_params* params,
+                              uint64_t first_packet, uint64_t n_packets, uint64_t seed,
+                              double* detector_dev, double* totals_dev, uint64_t* counters_dev,
+                              uint64_t* err_dev, double* flow_global_dev, double* flow_latitudinal_dev,
+                              void* stream);
 
 /* Duration in ms of the transport (all launches from emission to drain, without
  * the final detector reduction) of the most recent run on this grid, measured

@@ -109,6 +109,8 @@ typedef struct ctx {
     const double* th_weight; /* thermal: cell_weight [ncell] */
     double th_total;
     int th_cd0;            /* thermal: radial index of the first CDF entry (the computed cell_depth) */
+    double* flow_g;        /* thread-private [ncell][3] cell_flow_global, or NULL */
+    double* flow_t;        /* thread-private [ncell][4] cell_flow, or NULL */
 } ctx;
 
 static inline int cidx(const oracle_grid* g, const int c[3]) { return (c[2] * g->ntheta + c[1]) * g->nr + c[0]; }
@@ -986,6 +988,33 @@ static void emit_star(ctx* X, rng_t* rng, double pos[3], double dir[3], int face
     initial_cell(X, pos[0], pos[1], pos[2], cell);
 }
 
+/* add_flow_global (ARTES.f90:4992-5011): direction in the local (r, theta, phi) frame at
+ * the segment's end point x segment length x Stokes I */
+static void add_flow_global(ctx* X, const double pos[3], const double dir[3], double energy, double len,
+                            const int cell[3]) {
+    if (!X->flow_g) return;
+    double x = pos[0], y = pos[1], z = pos[2];
+    double theta = acos(z / sqrt(x * x + y * y + z * z));
+    double phi = atan2(y, x);
+    double r_dir = sin(theta) * cos(phi) * dir[0] + sin(theta) * sin(phi) * dir[1] + cos(theta) * dir[2];
+    double theta_dir = cos(theta) * cos(phi) * dir[0] + cos(theta) * sin(phi) * dir[1] - sin(theta) * dir[2];
+    double phi_dir = -sin(phi) * dir[0] + cos(phi) * dir[1];
+    double* f = X->flow_g + 3 * (size_t)cidx(X->g, cell);
+    f[0] += r_dir * len * energy;
+    f[1] += theta_dir * len * energy;
+    f[2] += phi_dir * len * energy;
+}
+
+/* add_flow (ARTES.f90:5013-5045) as called at a face crossing (728-743): 1 upward,
+ * 2 downward, 3 south, 4 north */
+static void add_flow_crossing(ctx* X, const int nf[2], const int cell[3], const int cout[3], double energy) {
+    if (!X->flow_t) return;
+    int d = 0;
+    if (nf[0] == 1) d = cout[0] > cell[0] ? 1 : cout[0] < cell[0] ? 2 : 0;
+    else if (nf[0] == 2) d = cout[1] > cell[1] ? 3 : cout[1] < cell[1] ? 4 : 0;
+    if (d) X->flow_t[4 * (size_t)cidx(X->g, cell) + d - 1] += energy;
+}
+
 /* propagation to the next interaction (ARTES.f90:689-778 / 848-941), with the surface:
  * absorption with probability 1 - surface_albedo, else Lambertian reflection and its peel
  * (ARTES.f90:753-774, 922-937); the optical depth keeps accumulating after a reflection.
@@ -1002,10 +1031,13 @@ static int propagate(ctx* X, rng_t* rng, double pos[3], double dir[3], int face[
         if (tau_run + tau_cell > tau) {
             double s = (tau - tau_run) / k;
             pos[0] += s * dir[0]; pos[1] += s * dir[1]; pos[2] += s * dir[2];
+            add_flow_global(X, pos, dir, st[0], s, cell);                 /* ARTES.f90:715, 874 */
             face[0] = 0; face[1] = 0;
             return 0;
         }
         pos[0] += fd * dir[0]; pos[1] += fd * dir[1]; pos[2] += fd * dir[2];
+        add_flow_global(X, pos, dir, st[0], fd, cell);                    /* ARTES.f90:728, 889 */
+        add_flow_crossing(X, nf, cell, cout, st[0]);                      /* ARTES.f90:730-743, 891-904 */
         face[0] = nf[0]; face[1] = nf[1];
         cell[0] = cout[0]; cell[1] = cout[1]; cell[2] = cout[2];
         if (gexit) return 1;
@@ -1108,8 +1140,19 @@ static int transport_packet(ctx* X, uint64_t seed, uint64_t id, double* nscat_ou
 
 /* Run packets [first, first+n). detector [4][4][ny][nx], totals[ARTES_NUM_TOTALS], counters, err are ACCUMULATED into.
  * records (optional) [n][4] = {peeled I sum, scatters, crossings, end state}. */
+int oracle_run_flow(const oracle_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
+                    int nthreads, double* detector, double* totals, uint64_t* counters, uint64_t* err, double* records,
+                    double* flow_global, double* flow_latitudinal);
+
 int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
                int nthreads, double* detector, double* totals, uint64_t* counters, uint64_t* err, double* records) {
+    return oracle_run_flow(g, p, first, n, seed, nthreads, detector, totals, counters, err, records, NULL, NULL);
+}
+
+/* oracle_run plus the flow accumulators (artes_run_flow layout, accumulated into; either may be NULL) */
+int oracle_run_flow(const oracle_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
+                    int nthreads, double* detector, double* totals, uint64_t* counters, uint64_t* err, double* records,
+                    double* flow_global, double* flow_latitudinal) {
     if (!g || !p || !detector) return -22;
     if (p->photon_source != 1 && p->photon_source != 2) return -22;
     double* th_cdf = NULL;
@@ -1137,7 +1180,11 @@ int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, 
     uint64_t* cnts = (uint64_t*)calloc((size_t)ARTES_NUM_COUNTERS * nthreads, sizeof(uint64_t));
     uint64_t* errs = (uint64_t*)calloc((size_t)ARTES_NUM_ERR * nthreads, sizeof(uint64_t));
     double* tots = (double*)calloc((size_t)ARTES_NUM_TOTALS * nthreads, sizeof(double));
-    if (!dets || !cnts || !errs || !tots) { free(dets); free(cnts); free(errs); free(tots); free(th_cdf); free(th_weight); return -12; }
+    const size_t nc = (size_t)g->ncell;
+    double* flows = (flow_global || flow_latitudinal) ? (double*)calloc(7 * nc * (size_t)nthreads, sizeof(double)) : NULL;
+    if (!dets || !cnts || !errs || !tots || ((flow_global || flow_latitudinal) && !flows)) {
+        free(dets); free(cnts); free(errs); free(tots); free(th_cdf); free(th_weight); free(flows); return -12;
+    }
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads)
 #endif
@@ -1160,6 +1207,8 @@ int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, 
         X.totals = tots + (size_t)ARTES_NUM_TOTALS * t;
         X.cur_pix = -1;
         X.th_cdf = th_cdf; X.th_weight = th_weight; X.th_total = th_total; X.th_cd0 = th_cd0;
+        X.flow_g = flow_global ? flows + 7 * nc * (size_t)t : NULL;
+        X.flow_t = flow_latitudinal ? flows + 7 * nc * (size_t)t + 3 * nc : NULL;
 #ifdef _OPENMP
 #pragma omp for schedule(static)
 #endif
@@ -1182,8 +1231,10 @@ int oracle_run(const oracle_grid* g, const artes_run_params* p, uint64_t first, 
         if (counters) for (int i = 0; i < ARTES_NUM_COUNTERS; i++) counters[i] += cnts[(size_t)ARTES_NUM_COUNTERS * t + i];
         if (err) for (int i = 0; i < ARTES_NUM_ERR; i++) err[i] += errs[(size_t)ARTES_NUM_ERR * t + i];
         if (totals) for (int i = 0; i < ARTES_NUM_TOTALS; i++) totals[i] += tots[(size_t)ARTES_NUM_TOTALS * t + i];
+        if (flow_global) for (size_t i = 0; i < 3 * nc; i++) flow_global[i] += flows[7 * nc * (size_t)t + i];
+        if (flow_latitudinal) for (size_t i = 0; i < 4 * nc; i++) flow_latitudinal[i] += flows[7 * nc * (size_t)t + 3 * nc + i];
     }
-    free(dets); free(cnts); free(errs); free(tots); free(th_cdf); free(th_weight);
+    free(dets); free(cnts); free(errs); free(tots); free(th_cdf); free(th_weight); free(flows);
     return 0;
 }
 

@@ -38,6 +38,8 @@ def lib():
         L.oracle_run.argtypes = [C.c_void_p, C.POINTER(RunParams), C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
                                  C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+        L.oracle_run_flow.restype = C.c_int
+        L.oracle_run_flow.argtypes = list(L.oracle_run.argtypes) + [C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.oracle_max_threads.restype = C.c_int
         dp = C.POINTER(C.c_double)
         L.oracle_thermal.restype = C.c_int
@@ -82,6 +84,24 @@ class OracleGrid:
         if rc != 0:
             raise RuntimeError(f"oracle_run failed: {rc}")
         return det, tot, cnt, err, rec
+
+    def run_flow(self, params: RunParams, first: int, n: int, seed: int, threads: int = 0):
+        """``run`` plus the flow accumulators: (det, totals, counters, err, flow_global
+        [nphi][ntheta][nr][3], flow_latitudinal [nphi][ntheta][nr][4])."""
+        a = self.arrays
+        det = np.zeros((4, 4, params.ny, params.nx))
+        tot = np.zeros(ARTES_NUM_TOTALS)
+        cnt = np.zeros(ARTES_NUM_COUNTERS, dtype=np.uint64)
+        err = np.zeros(ARTES_NUM_ERR, dtype=np.uint64)
+        fg = np.zeros((a.nphi, a.ntheta, a.nr, 3))
+        ft = np.zeros((a.nphi, a.ntheta, a.nr, 4))
+        dp, up = C.POINTER(C.c_double), C.POINTER(C.c_uint64)
+        rc = lib().oracle_run_flow(self.h, C.byref(params), first, n, seed, threads, det.ctypes.data_as(dp),
+                                   tot.ctypes.data_as(dp), cnt.ctypes.data_as(up), err.ctypes.data_as(up), None,
+                                   fg.ctypes.data_as(dp), ft.ctypes.data_as(dp))
+        if rc != 0:
+            raise RuntimeError(f"oracle_run_flow failed: {rc}")
+        return det, tot, cnt, err, fg, ft
 
     def close(self):
         if self.h:

@@ -21,7 +21,7 @@ def declared_functions():
 def test_header_declares_the_boundary():
     names = declared_functions()
     for required in ("artes_grid_create", "artes_grid_destroy", "artes_run", "artes_run_device",
-                     "artes_run_trace", "artes_last_kernel_ms", "artes_abi_version", "artes_grid_thermal"):
+                     "artes_run_trace", "artes_last_kernel_ms", "artes_abi_version", "artes_grid_thermal", "artes_run_flow", "artes_run_device_flow"):
         assert required in names
 
 
@@ -31,7 +31,7 @@ def test_library_exports_every_symbol():
     lib = engine.lib()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.artes_abi_version() == 2
+    assert lib.artes_abi_version() == 3
     assert b"gfx950" in lib.artes_build_info()
 
 

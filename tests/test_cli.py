@@ -49,7 +49,10 @@ class OracleTransport:
     def thermal(self, wl, thermal_weight, ring):
         return self.g.thermal(wl, thermal_weight, ring)
 
-    def run(self, params, first, n, seed):
+    def run(self, params, first, n, seed, flow_global=False, flow_latitudinal=False):
+        if flow_global or flow_latitudinal:
+            d, t, c, e, fg, ft = self.g.run_flow(params, first, n, seed, threads=4)
+            return RunResult(d, t, c, e, fg if flow_global else None, ft if flow_latitudinal else None)
         d, t, c, e, _ = self.g.run(params, first, n, seed, threads=4)
         return RunResult(d, t, c, e)
 
