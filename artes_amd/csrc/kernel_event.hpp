@@ -698,14 +698,15 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
     }
 }
 
-// initial fill: every slot is fresh and queued for emission
-__global__ void k_init(Pool S, int* emit, int* emit_n) {
+// initial fill: the first `use` slots are fresh and queued for emission (a run of fewer
+// packets than the pool holds leaves the rest untouched: no list ever names them)
+__global__ void k_init(Pool S, int* emit, int* emit_n, int use) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < S.P) {
+    if (i < use) {
         S.s[i].mode = S_FRESH;
         emit[i] = i;
     }
-    if (i == 0) *emit_n = S.P;
+    if (i == 0) *emit_n = use;
 }
 
 // end of an iteration: the output trace list (k_event's event_n entries, then k_emit's

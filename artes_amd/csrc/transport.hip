@@ -262,7 +262,11 @@ static bool use_event_engine() {
 static int32_t ensure_pool(artes_grid* g) {
     if (g->pool_mem) return 0;
     const char* env = getenv("ARTES_POOL");
-    long long P = env ? atoll(env) : (long long)g->num_cus * 16384;
+    // 64 Ki slots per CU (16.8 M, 4.3 GB on MI355X): every k_trace launch ends in a tail of
+    // a few long traces (~0.45 ms), so fewer, larger iterations pay it less often; beyond
+    // this the random slot accesses of k_event start to miss in the TLBs (pool sweep in
+    // DESIGN.md §3)
+    long long P = env ? atoll(env) : (long long)g->num_cus * 65536;
     P = std::max<long long>(1024, std::min<long long>(P, 1LL << 26));
     HIP_TRY(hipMalloc(&g->pool_mem, (size_t)P * sizeof(Slot)));
     g->pool.P = (int)P;
@@ -355,8 +359,9 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
         else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
     };
+    const int use = (int)std::min<uint64_t>((uint64_t)P, std::max<uint64_t>(R.n, 1));
     timed(g, ARTES_K_AUX, stream, [&] {
-        hipLaunchKernelGGL(k_init, dim3((P + 255) / 256), dim3(256), 0, stream, g->pool, g->d_emit, cnt + 3);
+        hipLaunchKernelGGL(k_init, dim3((use + 255) / 256), dim3(256), 0, stream, g->pool, g->d_emit, cnt + 3, use);
     });
     // pre-iteration: fill the pool; emitted packets go to trace list 0
     {
