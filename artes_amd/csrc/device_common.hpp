@@ -53,6 +53,7 @@ struct DevRun {
     int photon_source, photon_emission;
     double photon_bias;
     double det0, det1, det2, sdt, cdt, sdp, cdp;
+    double det_phi;                 // atan2(det1, det0) in [0, 2 pi] (peel_photon, ARTES.f90:4868-4870)
     double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
     double* __restrict__ det;       // [NCOPY][4][4][ny][nx]
     size_t det_stride;              // doubles per copy

@@ -347,9 +347,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             double phi_old = atan2(dy, dx);
             if (phi_old < 0.0) phi_old += TWO_PI;
             if (phi_old > TWO_PI) phi_old -= TWO_PI;
-            double phi_new = atan2(R.det1, R.det0);
-            if (phi_new < 0.0) phi_new += TWO_PI;
-            if (phi_new > TWO_PI) phi_new -= TWO_PI;
+            const double phi_new = R.det_phi;   // the detector's azimuth, once per run
             bool have_out = false;
             double so[4] = {0, 0, 0, 0};
             if (fabs(dz) < 1.0) {
@@ -455,8 +453,11 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
 //         HBM copy once at the end.  Float atomics to HBM execute at the memory side and
 //         stay in vmcnt for thousands of cycles, so every later load of the wave waited
 //         for them; the grid is one wave of resident blocks, each looping over many events.
+#ifndef ARTES_EVENT_WPE
+#define ARTES_EVENT_WPE 2
+#endif
 template <bool LDS_T, bool LDS_D>
-__global__ __launch_bounds__(BLOCK) void k_event(DevGrid G0, DevRun R, Pool S, Lists L) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, Lists L) {
     extern __shared__ double s_ev[];
     DevGrid G = G0;
     const size_t plane = (size_t)R.nx * R.ny;
@@ -562,8 +563,33 @@ __device__ __forceinline__ void emit_planet(const DevGrid& G, const DevRun& R, R
 // to position event_n + i of the output trace list (k_event filled [0, event_n)), a hole
 // (-1) when the ids have run out: list positions and packet ids need no atomics, and the
 // packet-to-slot assignment is deterministic.  k_rotate advances next_pkt and the count.
+// doubles of LDS k_emit stages for initial_cell: theta faces [ntheta+1], phi faces [nphi] + 2 pi
+__host__ __device__ inline size_t emit_table_doubles(int ntheta, int nphi) { return (size_t)ntheta + 1 + nphi + 1; }
+
+// the cell j of ascending faces f[0..n] with f[j] < v < f[j+1], or 0 when v sits on a face
+// or outside: the cell initial_cell's linear scan finds (ARTES.f90:2630-2660).  Binary
+// search: the scan's dependent loads were most of k_emit's time
+__device__ __forceinline__ int face_interval(const double* f, int n, double v) {
+    int lo = 0, hi = n - 1, j = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (f[mid] < v) { j = mid; lo = mid + 1; }
+        else hi = mid - 1;
+    }
+    return (j >= 0 && v < f[j + 1]) ? j : 0;
+}
+
 template <bool G3D, bool TRACE>
 __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lists L) {
+    extern __shared__ double s_em[];
+    double* s_tf = s_em;                      // theta faces
+    double* s_pf = s_em + (G.ntheta + 1);     // phi faces, then 2 pi
+    if constexpr (G3D) {
+        for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) s_tf[i] = G.thetaf[i];
+        for (int i = threadIdx.x; i < G.nphi; i += BLOCK) s_pf[i] = G.phif[i];
+        if (threadIdx.x == 0) s_pf[G.nphi] = TWO_PI;
+        __syncthreads();
+    }
     const int n = *L.emit_n;
     const int out0 = *L.event_n;
     const unsigned long long pkt0 = *L.next_pkt;
@@ -650,12 +676,8 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
             const double th = acos(pz / r);
             double ph = atan2(py, px);
             if (ph < 0.0) ph += TWO_PI;
-            for (int j = 0; j < G.ntheta; j++)
-                if (th > G.thetaf[j] && th < G.thetaf[j + 1]) { ct = j; break; }
-            for (int j = 0; j < G.nphi; j++) {
-                const double hi = (j < G.nphi - 1) ? G.phif[j + 1] : TWO_PI;
-                if (ph > G.phif[j] && ph < hi) { cp = j; break; }
-            }
+            ct = face_interval(s_tf, G.ntheta, th);
+            cp = face_interval(s_pf, G.nphi, ph);
         }
         }   // star
         S.s[slot].pid = pid;

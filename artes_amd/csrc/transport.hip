@@ -355,9 +355,10 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         L.grab = g->d_grab; L.next_pkt = g->d_next;
         return L;
     };
+    const size_t em_lds = G3D ? emit_table_doubles(G.ntheta, G.nphi) * sizeof(double) : 0;
     auto launch_emit = [&](const Lists& L) {
-        if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
-        else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+        if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), em_lds, stream, G, R, g->pool, L);
+        else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), em_lds, stream, G, R, g->pool, L);
     };
     const int use = (int)std::min<uint64_t>((uint64_t)P, std::max<uint64_t>(R.n, 1));
     timed(g, ARTES_K_AUX, stream, [&] {
@@ -482,6 +483,9 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.det1 = sin(p->det_theta) * sin(p->det_phi);
     R.det2 = cos(p->det_theta);
     R.sdt = sin(p->det_theta); R.cdt = cos(p->det_theta); R.sdp = sin(p->det_phi); R.cdp = cos(p->det_phi);
+    R.det_phi = atan2(R.det1, R.det0);
+    if (R.det_phi < 0.0) R.det_phi += 2.0 * M_PI;
+    if (R.det_phi > 2.0 * M_PI) R.det_phi -= 2.0 * M_PI;
     R.x_max = p->x_max; R.y_max = p->y_max; R.fstop = p->fstop; R.pmin = p->photon_minimum;
     R.surface_albedo = p->surface_albedo; R.theta_star = p->theta_star; R.phi_star = p->phi_star;
     R.det = g->d_copies; R.det_stride = stride;
