@@ -13,7 +13,7 @@ import numpy as np
 ARTES_NUM_ERR = 64
 ARTES_NUM_COUNTERS = 8
 ARTES_NUM_TOTALS = 10      # [0..3] sum T_p, [4..7] sum T_p^2, [8] flux_emitted, [9] flux_exit
-ARTES_ABI_VERSION = 3
+ARTES_ABI_VERSION = 4
 COUNTER_NAMES = ("crossings", "scatters", "peels", "packets", "exited", "absorbed", "dropped", "detected")
 
 _dp = C.POINTER(C.c_double)
@@ -36,7 +36,7 @@ class RunParams(C.Structure):
         ("det_theta", C.c_double), ("det_phi", C.c_double), ("x_max", C.c_double), ("y_max", C.c_double),
         ("fstop", C.c_double), ("photon_minimum", C.c_double), ("surface_albedo", C.c_double),
         ("theta_star", C.c_double), ("phi_star", C.c_double),
-        ("photon_emission", C.c_int32), ("thermal_weight", C.c_int32), ("ring", C.c_int32), ("reserved", C.c_int32),
+        ("photon_emission", C.c_int32), ("thermal_weight", C.c_int32), ("ring", C.c_int32), ("packet_moments", C.c_int32),
         ("photon_bias", C.c_double),
     ]
 

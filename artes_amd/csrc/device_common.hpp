@@ -51,6 +51,7 @@ struct DevRun {
     uint64_t first, n, seed;
     int nx, ny, photon_scattering, phase_far, stellar_direction, defer, refill, static_q64;
     int photon_source, photon_emission;
+    int moments;                    // accumulate packet-level moments (slot line 1, planes 12-15, tot2[0..3])
     double photon_bias;
     double det0, det1, det2, sdt, cdt, sdp, cdp;
     double det_phi;                 // atan2(det1, det0) in [0, 2 pi] (peel_photon, ARTES.f90:4868-4870)

@@ -33,12 +33,15 @@ namespace artes {
 
 // packet-state pool: one 256-byte record per slot (two 128-byte cache lines).  The
 // work lists visit slots in no particular order, so a record layout keeps every access
-// of a lane inside its own two lines; a structure-of-arrays pool would touch one line per
-// field per lane.  Line 0 holds what k_trace reads and writes, line 1 the event-only
-// state.  Every trace starts at the packet position (p*, pcell, pface) with zero
-// accumulated optical depth, so no separate trace position is stored.
+// of a lane inside its own lines; a structure-of-arrays pool would touch one line per
+// field per lane.  Line 0 holds the whole transport state: every kernel reads and writes
+// that line only.  Line 1 holds diagnostics -- the packet-level moments (R.moments),
+// the trace records (R.rec) -- and the rare surface-peel angle, so a production run moves
+// one random line per packet access instead of two.  Every trace starts at the packet
+// position (p*, pcell, pface) with zero accumulated optical depth, so no separate trace
+// position is stored.
 struct alignas(256) Slot {
-    // line 0: trace state
+    // line 0: transport state
     double px, py, pz;                  // packet position (last interaction / emission)
     double dx, dy, dz;                  // packet direction
     double ttgt;                        // target optical depth of a propagation trace
@@ -47,19 +50,18 @@ struct alignas(256) Slot {
     int mode, ncross;
     double wI;                          // Stokes I including the weights applied in k_trace
     double tpeel;                       // optical depth of the last peel-off trace
+    double q1, q2, q3;                  // Stokes Q, U, V per unit I as of the last scattering
+    // line 1: diagnostics and the surface peel
     double cos_surf;                    // surface peel: cos(normal, detector) (ARTES.f90:4623)
-    double spare0[2];
-    // line 1: event state
-    double s0, s1, s2, s3;              // Stokes vector as of the last scattering
-    double cs0, cs1, cs2, cs3;          // running contribution to the current pixel
-    double pt0, pt1, pt2, pt3;          // packet total per Stokes
+    double cs0, cs1, cs2, cs3;          // moments: running contribution to the current pixel
+    double pt0, pt1, pt2, pt3;          // moments: packet total per Stokes
     double peel_sum;                    // trace records: total peeled intensity
-    unsigned long long pid;
-    int cur_pix, nscat;
-    double spare1;
+    unsigned long long pid;             // trace records: packet id
+    int cur_pix, nscat;                 // moments: current pixel; trace records: scatterings
+    double spare1[4];
 };
 static_assert(sizeof(Slot) == 256, "slot record must be two cache lines");
-static_assert(offsetof(Slot, s0) == 128, "event state must start the second line");
+static_assert(offsetof(Slot, cos_surf) == 128, "line 0 must hold the whole transport state");
 
 struct Pool {
     int P;
@@ -239,19 +241,21 @@ __device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int s
     unsafeAtomicAdd(&acc[0 * plane + pix], v);
     unsafeAtomicAdd(&acc[4 * plane + pix], v * v);
     unsafeAtomicAdd(&acc[9 * plane + pix], 1.0);
-    const int cur = S.s[slot].cur_pix;
-    double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
-    if (pix != cur) {
-        if (cur >= 0) {
+    if (R.moments) {
+        const int cur = S.s[slot].cur_pix;
+        double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
+        if (pix != cur) {
+            if (cur >= 0) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
+                for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
+            }
+            S.s[slot].cur_pix = pix;
+            cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
         }
-        S.s[slot].cur_pix = pix;
-        cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
+        S.s[slot].cs0 = cs[0] + v; S.s[slot].cs1 = cs[1]; S.s[slot].cs2 = cs[2]; S.s[slot].cs3 = cs[3];
+        S.s[slot].pt0 += v;
     }
-    S.s[slot].cs0 = cs[0] + v; S.s[slot].cs1 = cs[1]; S.s[slot].cs2 = cs[2]; S.s[slot].cs3 = cs[3];
-    S.s[slot].pt0 += v;
-    S.s[slot].peel_sum += v;
+    if (R.rec) S.s[slot].peel_sum += v;
     c_det++;
 }
 
@@ -289,9 +293,8 @@ __device__ __forceinline__ int event_surface_hit(const DevGrid& G, const DevRun&
     direction_cosine(R, alpha, beta, n0, n1, n2, e0, e1, e2);
     S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
     S.s[slot].dx = e0; S.s[slot].dy = e1; S.s[slot].dz = e2;
-    // the surface depolarises (ARTES.f90:1396-1400); I carries k_trace's weights
-    const double wI = S.s[slot].wI;
-    S.s[slot].s0 = wI; S.s[slot].s1 = 0.0; S.s[slot].s2 = 0.0; S.s[slot].s3 = 0.0;
+    // the surface depolarises (ARTES.f90:1396-1400); I (wI) carries k_trace's weights
+    S.s[slot].q1 = 0.0; S.s[slot].q2 = 0.0; S.s[slot].q3 = 0.0;
     // cos of the angle between the surface normal and the detector (4623-4625)
     const double cos_angle = n0 * R.det0 + n1 * R.det1 + n2 * R.det2;
     S.s[slot].cos_surf = cos_angle;
@@ -327,9 +330,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         double dx = S.s[slot].dx, dy = S.s[slot].dy, dz = S.s[slot].dz;
         // k_trace scaled I by the forced-first-interaction and albedo weights (ARTES.f90:
         // 674-676, 801-807); the polarised components follow by the same factor
-        const double wI = S.s[slot].wI, sI = S.s[slot].s0;
-        const double f = (wI != sI && sI != 0.0) ? wI / sI : 1.0;
-        double st[4] = {wI, S.s[slot].s1 * f, S.s[slot].s2 * f, S.s[slot].s3 * f};
+        const double wI = S.s[slot].wI;
+        double st[4] = {wI, S.s[slot].q1 * wI, S.s[slot].q2 * wI, S.s[slot].q3 * wI};
         int cr, ct, cp;
         unpack_cell(S.s[slot].pcell, cr, ct, cp);
         const int cell = cr + G.nr * (ct + G.ntheta * cp);
@@ -382,26 +384,28 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                     } else {
                         const int pix = iy * R.nx + ix;
                         const double v[4] = {w * so[0], -w * so[1], w * so[2], w * so[3]};   // -Q: ARTES.f90:4956
-                        const int cur = S.s[slot].cur_pix;
-                        double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
-                        if (pix != cur) {
-                            if (cur >= 0) {
-#pragma unroll
-                                for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
-                            }
-                            S.s[slot].cur_pix = pix;
-                            cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
-                        }
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
                             unsafeAtomicAdd(&acc[q * plane + pix], v[q]);
                             unsafeAtomicAdd(&acc[(4 + q) * plane + pix], v[q] * v[q]);
-                            cs[q] += v[q];
                         }
                         unsafeAtomicAdd(&acc[8 * plane + pix], 1.0);
-                        S.s[slot].cs0 = cs[0]; S.s[slot].cs1 = cs[1]; S.s[slot].cs2 = cs[2]; S.s[slot].cs3 = cs[3];
-                        S.s[slot].pt0 += v[0]; S.s[slot].pt1 += v[1]; S.s[slot].pt2 += v[2]; S.s[slot].pt3 += v[3];
-                        S.s[slot].peel_sum += wI;
+                        if (R.moments) {   // packet-level moments (diagnostics, line 1)
+                            const int cur = S.s[slot].cur_pix;
+                            double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
+                            if (pix != cur) {
+                                if (cur >= 0) {
+#pragma unroll
+                                    for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
+                                }
+                                S.s[slot].cur_pix = pix;
+                                cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
+                            }
+                            S.s[slot].cs0 = cs[0] + v[0]; S.s[slot].cs1 = cs[1] + v[1];
+                            S.s[slot].cs2 = cs[2] + v[2]; S.s[slot].cs3 = cs[3] + v[3];
+                            S.s[slot].pt0 += v[0]; S.s[slot].pt1 += v[1]; S.s[slot].pt2 += v[2]; S.s[slot].pt3 += v[3];
+                        }
+                        if (R.rec) S.s[slot].peel_sum += wI;
                         c_det++;
                     }
                 } else {
@@ -412,7 +416,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         if (drop) { S.s[slot].mode = S_END_DROP; return 2; }
         // scatter_photon + polarization_rotation (ARTES.f90:819-846)
         c_scat++;
-        S.s[slot].nscat += 1;
+        if (R.rec) S.s[slot].nscat += 1;
         Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
         double alpha, beta;
         sample_angles(G, R, G.cums + (size_t)mid * CUM_DOUBLES, rng, st, alpha, beta);
@@ -423,7 +427,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         if (fabs(alpha) < 1.0) {
             double sn[4];
             polarization_rotation(R, alpha, beta, st, sc, dz, e2, sn, false);
-            S.s[slot].s0 = sn[0]; S.s[slot].s1 = sn[1]; S.s[slot].s2 = sn[2]; S.s[slot].s3 = sn[3];
+            const double inv = sn[0] != 0.0 ? 1.0 / sn[0] : 0.0;
+            S.s[slot].q1 = sn[1] * inv; S.s[slot].q2 = sn[2] * inv; S.s[slot].q3 = sn[3] * inv;
             S.s[slot].wI = sn[0];
             S.s[slot].dx = e0; S.s[slot].dy = e1; S.s[slot].dz = e2;
             const double xi = rng.uni();
@@ -607,16 +612,18 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
             if (m == S_END_EXIT) c_exit++;
             else if (m == S_END_ABS) c_abs++;
             else c_drop++;
-            const int cur = S.s[slot].cur_pix;
-            if (cur >= 0) {
-                unsafeAtomicAdd(&det[12 * plane + cur], S.s[slot].cs0 * S.s[slot].cs0);
-                unsafeAtomicAdd(&det[13 * plane + cur], S.s[slot].cs1 * S.s[slot].cs1);
-                unsafeAtomicAdd(&det[14 * plane + cur], S.s[slot].cs2 * S.s[slot].cs2);
-                unsafeAtomicAdd(&det[15 * plane + cur], S.s[slot].cs3 * S.s[slot].cs3);
+            if (R.moments) {
+                const int cur = S.s[slot].cur_pix;
+                if (cur >= 0) {
+                    unsafeAtomicAdd(&det[12 * plane + cur], S.s[slot].cs0 * S.s[slot].cs0);
+                    unsafeAtomicAdd(&det[13 * plane + cur], S.s[slot].cs1 * S.s[slot].cs1);
+                    unsafeAtomicAdd(&det[14 * plane + cur], S.s[slot].cs2 * S.s[slot].cs2);
+                    unsafeAtomicAdd(&det[15 * plane + cur], S.s[slot].cs3 * S.s[slot].cs3);
+                }
+                const double a0 = S.s[slot].pt0, a1 = S.s[slot].pt1, a2 = S.s[slot].pt2, a3 = S.s[slot].pt3;
+                t2[0] += a0 * a0; t2[1] += a1 * a1; t2[2] += a2 * a2; t2[3] += a3 * a3;
             }
             if (m == S_END_EXIT && R.photon_source == 2) f_exit += S.s[slot].wI;
-            const double a0 = S.s[slot].pt0, a1 = S.s[slot].pt1, a2 = S.s[slot].pt2, a3 = S.s[slot].pt3;
-            t2[0] += a0 * a0; t2[1] += a1 * a1; t2[2] += a2 * a2; t2[3] += a3 * a3;
             if constexpr (TRACE) {
                 double* rr = R.rec + (size_t)(S.s[slot].pid - R.first) * 4;
                 rr[0] = S.s[slot].peel_sum;
@@ -680,21 +687,26 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
             cp = face_interval(s_pf, G.nphi, ph);
         }
         }   // star
-        S.s[slot].pid = pid;
         S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
         S.s[slot].px = px; S.s[slot].py = py; S.s[slot].pz = pz;
         S.s[slot].dx = dx; S.s[slot].dy = dy; S.s[slot].dz = dz;
-        S.s[slot].s0 = wI; S.s[slot].s1 = 0.0; S.s[slot].s2 = 0.0; S.s[slot].s3 = 0.0;
+        S.s[slot].q1 = 0.0; S.s[slot].q2 = 0.0; S.s[slot].q3 = 0.0;
         S.s[slot].wI = wI;
         S.s[slot].pcell = pack_cell(cr, ct, cp); S.s[slot].pface = face;
         S.s[slot].ttgt = 0.0;
-        S.s[slot].cs0 = S.s[slot].cs1 = S.s[slot].cs2 = S.s[slot].cs3 = 0.0;
-        S.s[slot].pt0 = S.s[slot].pt1 = S.s[slot].pt2 = S.s[slot].pt3 = 0.0;
-        S.s[slot].peel_sum = 0.0;
-        S.s[slot].cur_pix = -1;
-        S.s[slot].nscat = 0;
+        S.s[slot].tpeel = 0.0;
         S.s[slot].ncross = 0;
         S.s[slot].mode = mode0;
+        if (R.moments) {
+            S.s[slot].cs0 = S.s[slot].cs1 = S.s[slot].cs2 = S.s[slot].cs3 = 0.0;
+            S.s[slot].pt0 = S.s[slot].pt1 = S.s[slot].pt2 = S.s[slot].pt3 = 0.0;
+            S.s[slot].cur_pix = -1;
+        }
+        if constexpr (TRACE) {
+            S.s[slot].pid = pid;
+            S.s[slot].peel_sum = 0.0;
+            S.s[slot].nscat = 0;
+        }
         }   // emit
         if (i < n) L.trace_out[out0 + i] = emit ? slot : -1;
     }

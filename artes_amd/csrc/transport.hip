@@ -472,6 +472,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.first = first; R.n = n; R.seed = seed;
     R.nx = p->nx; R.ny = p->ny; R.photon_scattering = p->photon_scattering; R.phase_far = p->phase_far;
     R.photon_source = p->photon_source; R.photon_emission = p->photon_emission; R.photon_bias = p->photon_bias;
+    R.moments = p->packet_moments != 0 || rec != nullptr;
     R.stellar_direction = p->stellar_direction;
     const char* env = getenv("ARTES_DEFER");
     R.defer = env ? atoi(env) : 16;

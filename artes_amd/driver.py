@@ -304,8 +304,12 @@ def write_error_log(path: str, err_counts) -> None:
 
 
 def run_params(cfg: RunConfig, det: Detector, wl_index: int = 0, det_phi: float | None = None,
-               cell_depth: int = -1):
-    """Pack the globals ``radiative_transfer`` reads into the C-ABI ``artes_run_params``."""
+               cell_depth: int = -1, packet_moments: bool = True):
+    """Pack the globals ``radiative_transfer`` reads into the C-ABI ``artes_run_params``.
+
+    ``packet_moments``: also accumulate the packet-level second moments (detector planes
+    12-15, totals[4:8]) that the honest-error statistics (``stats.py``) need.  The
+    reference's outputs do not use them; the drop-in CLI and the bench turn them off."""
     from .abi import RunParams
 
     phi = det.det_phi if det_phi is None else det_phi
@@ -318,7 +322,7 @@ def run_params(cfg: RunConfig, det: Detector, wl_index: int = 0, det_phi: float 
         fstop=float(cfg.fstop), photon_minimum=float(cfg.photon_minimum), surface_albedo=float(cfg.surface_albedo),
         theta_star=float(cfg.theta_star), phi_star=float(cfg.phi_star),
         photon_emission=int(cfg.photon_emission), thermal_weight=int(bool(cfg.thermal_weight)),
-        ring=int(bool(cfg.ring)), reserved=0, photon_bias=float(cfg.photon_bias))
+        ring=int(bool(cfg.ring)), packet_moments=int(bool(packet_moments)), photon_bias=float(cfg.photon_bias))
 
 
 def default_config() -> RunConfig:

@@ -172,7 +172,7 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
         flows["flow_latitudinal"] = True
 
     def transport_call(wl: int, det_phi: float):
-        params = driver.run_params(cfg, det, wl, det_phi=det_phi, cell_depth=source(wl)[0])
+        params = driver.run_params(cfg, det, wl, det_phi=det_phi, cell_depth=source(wl)[0], packet_moments=False)
         base = call[0] * packages
         call[0] += 1
         res = dist.run_sharded(lambda first, n, s: transport.run(params, base + first, n, s, **flows), packages, seed, r)

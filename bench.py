@@ -80,7 +80,9 @@ def main() -> int:
     rtop = float(atm["radial"][-1])
     det_geom = driver.detector_geometry(cfg, rtop)
     grid = Grid(atm, device=dev)
-    params = driver.run_params(cfg, det_geom, 0, cell_depth=grid.cell_depth(0))
+    # the timed steps run the drop-in's production configuration: no packet-level moments
+    # (the reference has none); the parity check below reruns one step with them
+    params = driver.run_params(cfg, det_geom, 0, cell_depth=grid.cell_depth(0), packet_moments=False)
     ny, nx = det_geom.ny, det_geom.nx
 
     f64 = dict(dtype=torch.float64, device=f"cuda:{dev}")
@@ -149,6 +151,7 @@ def main() -> int:
     total_packets = per_gpu * world * args.steps
     value = total_packets / elapsed / 1e6
     cnt_h = cnt.cpu().numpy().astype(np.float64)
+    err_h = err.cpu().numpy()
     n_step = per_gpu * world
     C = cnt_h[0] / n_step
     S = cnt_h[1] / n_step
@@ -169,18 +172,24 @@ def main() -> int:
         except Exception:
             traffic = None
 
-    # Stokes-I parity against the frozen reference run (tests/golden)
+    # Stokes-I parity against the frozen reference run (tests/golden): one more step of the
+    # same workload, untimed, with the packet-level moments the honest per-pixel errors need
     parity = None
     ref_dir = os.path.join(ROOT, "tests", "golden", "reference_runs", "t_ray3d_ARTES_det_1e6")
     if os.path.isdir(ref_dir):
+        check = driver.run_params(cfg, det_geom, 0, cell_depth=grid.cell_depth(0), packet_moments=True)
+        det.zero_(); tot2.zero_()
+        grid.run_device(check, 0, per_gpu, args.seed + 1, det.data_ptr(), tot2.data_ptr(), 0, 0, stream.cuda_stream)
+        torch.cuda.synchronize()
         raw = det.cpu().numpy()
-        E = driver.package_energy(cfg, float(atm["wavelength"][0]) * 1e-6, rtop, n_step, det_geom.det_phi)
-        cmp = stats.compare_to_reference(raw, n_step, E, det_geom.pixel_scale, stats.load_reference_run(ref_dir), 10**6)
+        E = driver.package_energy(cfg, float(atm["wavelength"][0]) * 1e-6, rtop, per_gpu, det_geom.det_phi)
+        cmp = stats.compare_to_reference(raw, per_gpu, E, det_geom.pixel_scale, stats.load_reference_run(ref_dir), 10**6)
         ph = driver.photometry(driver.scale_detector(raw[:3], E))
         ref_ph = stats.load_reference_run(ref_dir)["photometry"]
         parity = {"stokes_I_rms_z": round(cmp["rms_z"], 4), "stokes_I_mean_z": round(cmp["mean_z"], 4),
                   "pixels": cmp["n_pixels"], "I_total": ph[0] * 1e-6, "I_total_reference": float(ref_ph[1]),
-                  "reference": "tests/golden/reference_runs/t_ray3d_ARTES_det_1e6 (1e6 packets)"}
+                  "reference": "tests/golden/reference_runs/t_ray3d_ARTES_det_1e6 (1e6 packets)",
+                  "sample": f"{per_gpu} packets on rank 0, untimed, packet moments on"}
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -211,7 +220,7 @@ def main() -> int:
                      "events_per_packet": {"crossings": round(C, 3), "scatters": round(S, 4), "peels": round(P, 4)}},
         "cpu_baseline": cpu,
         "parity": parity,
-        "errors": {str(i): int(e) for i, e in enumerate(err.cpu().numpy()) if e},
+        "errors": {str(i): int(e) for i, e in enumerate(err_h) if e},
     }
     print(json.dumps(out), flush=True)
     if world > 1:

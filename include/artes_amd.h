@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define ARTES_ABI_VERSION 3
+#define ARTES_ABI_VERSION 4
 #define ARTES_NUM_TOTALS 10
 #define ARTES_NUM_ERR 64
 
@@ -96,7 +96,10 @@ typedef struct artes_run_params {
     int32_t photon_emission; /* 1 = isotropic, 2 = biased upward (photon:emission)  */
     int32_t thermal_weight;  /* photon:weight: cell luminosity weighting on/off     */
     int32_t ring;            /* planet:ring (thermal cell_depth skips 2 cells)      */
-    int32_t reserved;
+    int32_t packet_moments;  /* 1: also accumulate the packet-level second moments
+                              * (detector planes 12-15, totals[4..7]) for honest
+                              * Monte-Carlo errors; 0: skip them (the reference has
+                              * none, and they double the per-event slot traffic)     */
     double photon_bias;      /* photon:bias, 0 <= b < 1                             */
 } artes_run_params;
 

@@ -31,7 +31,7 @@ def test_library_exports_every_symbol():
     lib = engine.lib()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.artes_abi_version() == 3
+    assert lib.artes_abi_version() == 4
     assert b"gfx950" in lib.artes_build_info()
 
 

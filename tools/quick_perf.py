@@ -30,9 +30,12 @@ for name in ("ray3d", "hg", "iso"):
     for env in variants:
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        g.run(p, 0, 10**5, 1)
+        # QP_MOMENTS=0: production configuration without packet-level moments
+        pv = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0),
+                               packet_moments=os.environ.get("QP_MOMENTS", "1") == "1")
+        g.run(pv, 0, 10**5, 1)
         g.kernel_times()
-        g.run(p, 0, n, 2024)
+        g.run(pv, 0, n, 2024)
         kt = g.kernel_times()
         ms = g.last_kernel_ms()
         print(f"  {name} {env}: {ms:.1f} ms -> {n / ms * 1e3:.4g} pkt/s  "
