@@ -64,6 +64,25 @@ def test_launch_knobs_do_not_change_results(require_gpu, knobs):
     np.testing.assert_allclose(base.totals, other.totals, rtol=1e-9)
 
 
+def test_packet_moments_are_pure_diagnostics(require_gpu):
+    """packet_moments = 0 (the CLI / bench setting) transports the same packets: every
+    detector plane the reference writes, the counters and the fluxes are identical; only
+    the packet-level moment planes 12-15 and totals[4:8] stay empty."""
+    atm = synthetic.make_config("ray3d", nr=10, ntheta=6, nphi=8)
+    cfg = driver.default_config()
+    det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
+    from artes_amd.engine import Grid
+
+    grid = Grid(atm, device=0)
+    on = grid.run(driver.run_params(cfg, det, 0, cell_depth=-1, packet_moments=True), 0, 200000, 5)
+    off = grid.run(driver.run_params(cfg, det, 0, cell_depth=-1, packet_moments=False), 0, 200000, 5)
+    np.testing.assert_array_equal(on.counters, off.counters)
+    np.testing.assert_allclose(off.det[:3], on.det[:3], rtol=1e-9, atol=1e-300)
+    assert np.all(off.det[3] == 0) and on.det[3].sum() > 0
+    np.testing.assert_allclose(off.totals[:4], on.totals[:4], rtol=1e-9)
+    assert np.all(off.totals[4:8] == 0) and on.totals[4] > 0
+
+
 def test_kernel_times_profiling(require_gpu):
     atm, grid, p = _setup()
     assert grid.kernel_times()["trace"] == (0.0, 0)          # profiling off: nothing recorded
