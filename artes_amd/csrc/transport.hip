@@ -477,7 +477,11 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     const char* env = getenv("ARTES_DEFER");
     R.defer = env ? atoi(env) : 16;
     const char* rf = getenv("ARTES_REFILL");
-    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : 32;
+    // refill a wave once this many of its lanes are idle: a 3D step (one of three face
+    // families) costs more than a radial-only one, so idle lanes are worth refilling sooner
+    // (ray3d best at 24, radial-only grids at 28-32)
+    const bool grid3d = (T.ntheta > 1 || T.nphi > 1);
+    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? 24 : 32);
     const char* sq = getenv("ARTES_STATIC");   // statically split share of the trace list, in 1/64
     R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : 32;
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)
