@@ -335,7 +335,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         int cr, ct, cp;
         unpack_cell(S.s[slot].pcell, cr, ct, cp);
         const int cell = cr + G.nr * (ct + G.ntheta * cp);
-        const int mid = G.matid[cell];
+        const int mid = G.nmat == 1 ? 0 : G.matid[cell];   // uniform atmosphere: no dependent load
         const double* __restrict__ P = G.mats + (size_t)mid * MAT_DOUBLES;
         const double tau_peel = S.s[slot].tpeel;
         bool drop = false;
