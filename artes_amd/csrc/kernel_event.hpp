@@ -68,8 +68,14 @@ struct Pool {
     Slot* __restrict__ s;
 };
 
+// A trace list is read as list index j < split -> position j, j >= split -> position
+// P-1-(j-split).  Two orders (R.emit_first):
+//  0: k_event's traces at [0, event_n), k_emit's after them (split = the whole list);
+//  1: k_emit's traces at the front, k_event's from position P-1 downwards (split =
+//     emit_n): the new packets' chains (first optical depth -> propagation -> peel) are
+//     handed out first.  Radial-only grids gain 2-6 % from it, ray3d loses 1.5 %.
 struct Lists {
-    const int* trace_in;  const int* trace_in_n;
+    const int* trace_in;  const int* trace_in_n;  const int* trace_in_split;
     int* trace_out;       int* trace_out_n;
     int* event;           int* event_n;
     int* emit;            int* emit_n;
@@ -494,7 +500,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
         const int dest = slot >= 0 ? event_one(G, R, S, slot, det, acc, plane, c_scat, c_det) : 0;
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
-        if (i < n) L.trace_out[i] = (dest == 1) ? slot : -1;
+        if (i < n) L.trace_out[R.emit_first ? S.P - 1 - i : i] = (dest == 1) ? slot : -1;
         wave_append(dest == 2, slot, L.emit, L.emit_n);
     }
     if constexpr (LDS_D) {
@@ -565,8 +571,8 @@ __device__ __forceinline__ void emit_planet(const DevGrid& G, const DevRun& R, R
 // close finished packets and emit new ones (ARTES.f90:546-597, 1027-1115, 2605-2669)
 //
 // Emit-list entry i takes packet id next_pkt + i (ids < n only) and writes its new trace
-// to position event_n + i of the output trace list (k_event filled [0, event_n)), a hole
-// (-1) when the ids have run out: list positions and packet ids need no atomics, and the
+// to position out0 + i of the output trace list (see Lists), a hole (-1)
+// when the ids have run out: list positions and packet ids need no atomics, and the
 // packet-to-slot assignment is deterministic.  k_rotate advances next_pkt and the count.
 // doubles of LDS k_emit stages for initial_cell: theta faces [ntheta+1], phi faces [nphi] + 2 pi
 __host__ __device__ inline size_t emit_table_doubles(int ntheta, int nphi) { return (size_t)ntheta + 1 + nphi + 1; }
@@ -596,7 +602,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         __syncthreads();
     }
     const int n = *L.emit_n;
-    const int out0 = *L.event_n;
+    const int out0 = R.emit_first ? 0 : *L.event_n;
     const unsigned long long pkt0 = *L.next_pkt;
     const size_t plane = (size_t)R.nx * R.ny;
     double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
@@ -746,11 +752,12 @@ __global__ void k_init(Pool S, int* emit, int* emit_n, int use) {
 // end of an iteration: the output trace list (k_event's event_n entries, then k_emit's
 // emit_n) becomes the input, the consumed input buffer is reset to become the next
 // output, packet ids advance by the emit-list length; event/emit lists and cursors are zeroed
-__global__ void k_rotate(int* in_n, int* out_n, int* event_n, int* emit_n, unsigned int* grab,
-                         unsigned long long* next_pkt) {
+__global__ void k_rotate(int* in_n, int* out_n, int* out_split, int* event_n, int* emit_n, unsigned int* grab,
+                         unsigned long long* next_pkt, int emit_first) {
     if (threadIdx.x == 0) {
         const int ev = *event_n, em = *emit_n;
         *out_n = ev + em;
+        *out_split = emit_first ? em : ev + em;
         *next_pkt += (unsigned long long)em;
         *in_n = 0;
         *event_n = 0;

@@ -213,6 +213,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     extern __shared__ double s_tab[];
     const TraceTabs T = stage_trace_tables(G, s_tab);
     const int n = *L.trace_in_n;
+    const int split = *L.trace_in_split;   // [0, split): new packets' traces; then k_event's, stored backwards
     const int home = blockIdx.x & 7;
     __shared__ int s_q[2][BLOCK];
     const int wbase = threadIdx.x & ~63;
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
                 dbg_refills++;
 #endif
-                if (!have && my >= 0) slot = L.trace_in[my];
+                if (!have && my >= 0) slot = L.trace_in[my < split ? my : S.P - 1 - (my - split)];
                 if (!have && my >= 0 && slot >= 0) {   // -1: a hole left by a dropped or retired packet
                     const Slot* rec = S.s + slot;
                     mode = rec->mode;

@@ -348,7 +348,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     }
     auto lists = [&](int in) {
         Lists L;
-        L.trace_in = g->d_lists[in]; L.trace_in_n = cnt + in;
+        L.trace_in = g->d_lists[in]; L.trace_in_n = cnt + in; L.trace_in_split = cnt + 4 + in;
         L.trace_out = g->d_lists[1 - in]; L.trace_out_n = cnt + (1 - in);
         L.event = g->d_event; L.event_n = cnt + 2;
         L.emit = g->d_emit; L.emit_n = cnt + 3;
@@ -369,7 +369,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         Lists L = lists(1);   // trace_out = list 0
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
-            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + 1, cnt + 0, cnt + 2, cnt + 3, g->d_grab, g->d_next);
+            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + 1, cnt + 0, cnt + 4 + 0, cnt + 2, cnt + 3, g->d_grab, g->d_next,
+                               R.emit_first);
         });
     }
     HIP_TRY(hipGetLastError());
@@ -387,7 +388,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         });
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
-            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + in, cnt + (1 - in), cnt + 2, cnt + 3, g->d_grab, g->d_next);
+            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + in, cnt + (1 - in), cnt + 4 + (1 - in), cnt + 2, cnt + 3,
+                               g->d_grab, g->d_next, R.emit_first);
         });
         in = 1 - in;
         it++;
@@ -482,6 +484,8 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // (ray3d best at 24, radial-only grids at 28-32)
     const bool grid3d = (T.ntheta > 1 || T.nphi > 1);
     R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? 24 : 32);
+    const char* ef = getenv("ARTES_EMIT_FIRST");
+    R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
     const char* sq = getenv("ARTES_STATIC");   // statically split share of the trace list, in 1/64
     R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : 32;
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)

@@ -49,7 +49,8 @@ def test_event_and_persistent_engines_agree(require_gpu):
 
 
 @pytest.mark.parametrize("knobs", [dict(ARTES_POOL="5000"), dict(ARTES_REFILL="1", ARTES_STATIC="0"),
-                                   dict(ARTES_REFILL="64", ARTES_STATIC="64"), dict(ARTES_LDS="0", ARTES_WPE="4")])
+                                   dict(ARTES_REFILL="64", ARTES_STATIC="64"), dict(ARTES_LDS="0", ARTES_WPE="4"),
+                                   dict(ARTES_EMIT_FIRST="0"), dict(ARTES_EMIT_FIRST="1", ARTES_POOL="3000")])
 def test_launch_knobs_do_not_change_results(require_gpu, knobs):
     """Pool size, refill policy, trace-list split, LDS staging and occupancy only change
     the schedule: per-packet histories and all counters are identical."""
