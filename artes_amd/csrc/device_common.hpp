@@ -53,6 +53,7 @@ struct DevRun {
     int photon_source, photon_emission;
     int moments;                    // accumulate packet-level moments (slot line 1, planes 12-15, tot2[0..3])
     int emit_first;                 // trace-list order (kernel_event.hpp, Lists)
+    int backward;                   // k_trace: backward propagation after the forced interaction
     double photon_bias;
     double det0, det1, det2, sdt, cdt, sdp, cdp;
     double det_phi;                 // atan2(det1, det0) in [0, 2 pi] (peel_photon, ARTES.f90:4868-4870)

@@ -236,6 +236,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     double m0 = NONE, m1 = NONE, m2 = NONE;
     int sides = 0;
     uint32_t c_cross = 0, c_peel = 0;
+    // backward propagation after the forced first interaction (see the FIRST-trace end).
+    // During a first trace: the packet's crossings when it started.  During the backward
+    // trace that may follow: 2 x crossings at its start + the first trace's steps + 1
+    // (from which the forward walk's step count follows at the interaction).  0 otherwise.
+    int kb = 0;
 
     // a trace starts at the packet position with zero optical depth
     auto start_trace = [&](double d0, double d1, double d2) {
@@ -272,6 +277,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     const bool peel = is_peel_trace(mode);
                     start_trace(peel ? R.det0 : ldx, peel ? R.det1 : ldy, peel ? R.det2 : ldz);
                     have = true;
+                    kb = (mode == S_FIRST) ? ncross : 0;
                 }
             }
         }
@@ -375,6 +381,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     px = tx + s * nx; py = ty + s * ny; pz = tz + s * nz;
                     pcell = pack_cell(tcr, tct, tcp);
                     pface = 0;
+                    if (kb) {   // a backward trace: count the steps the forward one takes
+                        c_cross += (uint32_t)(kb - 2 * ncross);
+                        ncross = kb - ncross;
+                        kb = 0;
+                    }
                     if constexpr (FLOW) flow_segment(R.flow_g, R.flow_t, cell, px, py, pz, nx, ny, nz, s, wI, -1);   // (715, 874)
                     const double xi = rng.uni();   // a killed packet's RNG state is not used again
                     bool kill = !R.photon_scattering || xi < R.fstop;
@@ -424,9 +435,30 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         const double e = mid ? 1.0 - exp(-tau_first) : 1.0;
                         const double tau = -log(1.0 - xi * e);
                         if (mid) wI *= e;
-                        ttgt = tau;
                         mode = S_PROP;
-                        start_trace(nx, ny, nz);
+                        // The propagation that follows walks the first trace's chord again, from
+                        // its start to optical depth tau (ARTES.f90:689-720).  When the
+                        // interaction lies in the chord's far half it is reached in fewer cells
+                        // from the far end: walk back from where the first trace stopped to
+                        // optical depth tau_first - tau.  Same cells in reverse, so the same
+                        // interaction point up to rounding; crossing counts are kept as the
+                        // forward walk's (bfix).  Not with the flow diagnostics (segment order).
+                        bool back = false;
+                        if constexpr (!FLOW) back = R.backward && mid && !err && tau_first - tau < tau;
+                        kb = back ? 2 * ncross + (ncross - kb) + 1 : 0;
+                        if (back) {
+                            ttgt = fmax(tau_first - tau, 0.0);   // tau rounds to <= tau_first + 1 ulp
+                            tx += best * nx; ty += best * ny; tz += best * nz;
+                            tft = nft; tfi = nfi;
+                            nx = -nx; ny = -ny; nz = -nz;
+                            tacc = 0.0;
+                            tpar = 0.0;
+                            pending = fam_all;
+                            if constexpr (G3D) inz = fast_rcp(nz);
+                        } else {
+                            ttgt = tau;
+                            start_trace(nx, ny, nz);
+                        }
                     }
                 }
                 if (end) {   // write the packet state back once

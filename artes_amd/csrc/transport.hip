@@ -486,6 +486,8 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? 24 : 32);
     const char* ef = getenv("ARTES_EMIT_FIRST");
     R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
+    const char* bw = getenv("ARTES_BACKWARD");
+    R.backward = bw ? (atoi(bw) != 0) : 1;
     const char* sq = getenv("ARTES_STATIC");   // statically split share of the trace list, in 1/64
     R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : 32;
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)

@@ -65,6 +65,24 @@ def test_launch_knobs_do_not_change_results(require_gpu, knobs):
     np.testing.assert_allclose(base.totals, other.totals, rtol=1e-9)
 
 
+@pytest.mark.parametrize("name,spec", [("hg", {}), ("ray3d", dict(nr=10, ntheta=6, nphi=8, tau=3.0))])
+def test_backward_propagation_matches_forward(require_gpu, name, spec):
+    """The propagation after the forced first interaction may walk the chord back from
+    its far end (kernel_trace.hpp): same interaction point up to rounding, and the
+    per-packet crossing counts are reported as the forward walk's."""
+    atm, grid, p = _setup(name, **spec)
+    back = grid.trace(p, 0, 20000, 31)
+    with _env(ARTES_BACKWARD="0"):
+        fwd = grid.trace(p, 0, 20000, 31)
+    same = (np.isclose(back[:, 0], fwd[:, 0], rtol=1e-9, atol=1e-300) & (back[:, 1] == fwd[:, 1])
+            & (back[:, 2] == fwd[:, 2]) & (back[:, 3] == fwd[:, 3]))
+    assert same.mean() >= 0.999
+    with _env(ARTES_BACKWARD="0"):
+        c_fwd = grid.run(p, 0, 200000, 8).counter("crossings")
+    c_back = grid.run(p, 0, 200000, 8).counter("crossings")
+    assert c_back == pytest.approx(c_fwd, rel=1e-3)
+
+
 def test_packet_moments_are_pure_diagnostics(require_gpu):
     """packet_moments = 0 (the CLI / bench setting) transports the same packets: every
     detector plane the reference writes, the counters and the fluxes are identical; only
