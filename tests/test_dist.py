@@ -29,13 +29,15 @@ g = OracleGrid(atm)
 p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0))
 
 def transport(first, n, seed):
-    d, t, c, e, _ = g.run(p, first, n, seed, threads=2)
-    return RunResult(d, t, c, e)
+    d, t, c, e, fg, ft = g.run_flow(p, first, n, seed, threads=2)
+    return RunResult(d, t, c, e, fg, ft)
 
 res = dist.run_sharded(transport, 30001, 99, r)
 if r.rank == 0:
     np.save({out!r}, res.det)
     np.save({out!r}.replace(".npy", "_cnt.npy"), res.counters)
+    np.save({out!r}.replace(".npy", "_flow.npy"), res.flow_global)
+    np.save({out!r}.replace(".npy", "_lat.npy"), res.flow_latitudinal)
 tdist.barrier()
 tdist.destroy_process_group()
 '''
@@ -69,6 +71,9 @@ def test_two_rank_gloo_equals_single_process(tmp_path):
     det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
     g = OracleGrid(atm)
     p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0))
-    d1, _, c1, _, _ = g.run(p, 0, 30001, 99, threads=4)
+    d1, _, c1, _, fg1, ft1 = g.run_flow(p, 0, 30001, 99, threads=4)
     np.testing.assert_allclose(det2, d1, rtol=1e-11, atol=1e-300)
     np.testing.assert_array_equal(cnt2, c1)
+    # the flow diagnostics are summed over the ranks too
+    np.testing.assert_allclose(np.load(out.replace(".npy", "_flow.npy")), fg1, rtol=1e-10, atol=1e-12 * np.abs(fg1).max())
+    np.testing.assert_allclose(np.load(out.replace(".npy", "_lat.npy")), ft1, rtol=1e-11, atol=1e-300)
