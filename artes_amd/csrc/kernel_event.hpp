@@ -246,7 +246,7 @@ __device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int s
     if (pix < 0) { log_err(R, 63); return; }
     unsafeAtomicAdd(&acc[0 * plane + pix], v);
     unsafeAtomicAdd(&acc[4 * plane + pix], v * v);
-    unsafeAtomicAdd(&acc[9 * plane + pix], 1.0);
+    unsafeAtomicAdd(&det[9 * plane + pix], 1.0);   // rare (thermal / surface): straight to the block's HBM copy
     if (R.moments) {
         const int cur = S.s[slot].cur_pix;
         double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
@@ -320,7 +320,7 @@ __device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S
 }
 
 // one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended)
-// `acc` takes planes 0-9 (I Q U V sums, their squares, the peel count, the I-only count)
+// `acc` takes planes 0-8 (I Q U V sums, their squares, the peel count)
 // at plane stride `plane`:
 // the block's LDS detector or the global copy; `det` (global) takes moments 12-15
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
@@ -460,7 +460,7 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
 //  LDS_T: the scattering tables (one 31 KB set per distinct matrix) are staged in LDS --
 //         the angle sampling is two binary searches whose every probe depends on the
 //         previous one, so each probe's latency (LDS ~100 cycles, L2 ~500) is paid in full.
-//  LDS_D: the block accumulates planes 0-9 of the detector in LDS and adds them to its
+//  LDS_D: the block accumulates planes 0-8 of the detector in LDS and adds them to its
 //         HBM copy once at the end.  Float atomics to HBM execute at the memory side and
 //         stay in vmcnt for thousands of cycles, so every later load of the wave waited
 //         for them; the grid is one wave of resident blocks, each looping over many events.
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
     double* __restrict__ acc = det;
     if constexpr (LDS_D) {
         acc = lds_next;
-        for (size_t i = threadIdx.x; i < 10 * plane; i += BLOCK) acc[i] = 0.0;
+        for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) acc[i] = 0.0;
     }
     if constexpr (LDS_T || LDS_D) __syncthreads();
     const int n = *L.event_n;
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
     }
     if constexpr (LDS_D) {
         __syncthreads();
-        for (size_t i = threadIdx.x; i < 10 * plane; i += BLOCK) {
+        for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) {
             const double v = acc[i];
             if (v != 0.0) unsafeAtomicAdd(&det[i], v);
         }

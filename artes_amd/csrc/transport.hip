@@ -332,8 +332,10 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const size_t ev_bytes = event_table_doubles(G.nmat) * sizeof(double);
     const char* el = getenv("ARTES_EVENT_LDS");
     const bool ev_lds = (el ? atoi(el) != 0 : true) && ev_bytes <= 65536;
-    // detector planes 0-9 accumulated per k_event block in LDS when they fit
-    const size_t det_bytes = 10 * (size_t)R.nx * R.ny * sizeof(double);
+    // planes 0-8 of the detector accumulated per k_event block in LDS when they fit
+    // (the I-only count plane 9 of the rare thermal / surface peels goes straight to HBM):
+    // with the scattering tables, 76.7 KB at 25x25 pixels, so two blocks share a CU
+    const size_t det_bytes = 9 * (size_t)R.nx * R.ny * sizeof(double);
     const char* dl = getenv("ARTES_DET_LDS");
     const bool det_lds = (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
     int ev_blocks = side_blocks;
@@ -403,7 +405,9 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         if (it > max_it) return fail(-5, "event engine did not terminate");
     }
     g->last_iterations = it;
-    if (getenv("ARTES_VERBOSE")) fprintf(stderr, "[artes] event engine: pool %d, %lld iterations, trace blocks %d\n", P, it, g->trace_blocks);
+    if (getenv("ARTES_VERBOSE"))
+        fprintf(stderr, "[artes] event engine: pool %d, %lld iterations, trace blocks %d, event blocks %d (LDS tables %d, detector %d)\n",
+                P, it, g->trace_blocks, ev_blocks, (int)ev_lds, (int)det_lds);
     return 0;
 }
 
