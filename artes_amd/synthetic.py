@@ -18,6 +18,8 @@ config     scattering                                      grid (r x theta x phi
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from . import opacity as op
@@ -74,6 +76,63 @@ def make_config(name: str, **over) -> dict:
     spec = dict(CONFIGS[name])
     spec.update(over)
     return make(**spec)
+
+
+CLOUDY_IN = """[grid]
+radius: 1.
+radial:
+theta: 30, 60, 90, 120, 150
+phi: 60, 120, 180, 240, 300
+
+[composition]
+gas: on
+molweight: 2.3
+log_g: 3.4
+fits01: cloud.fits
+opacity01: 1, {cloud_density}, 4, 12, 1, 4, 0, 3
+ring:
+"""
+
+
+def make_cloudy(directory: str, wavelength=(0.5, 0.7, 0.9), levels: int = 17, p_max: float = 10.0,
+                cloud_density: float = 5e-13, gas_absorption: float = 0.05) -> dict:
+    """BASELINE configs[3]'s input shape, scaled down: a gas atmosphere with a Mie cloud
+    patch, several wavelengths, built through the reference's own setup path.
+
+    Writes ``directory`` = ``input/<atm>/`` as a user of ``python/atmosphere.py`` would:
+    an isothermal ``pressureTemperature.dat`` (``pressureTemperatureIsothermal.py``),
+    one gas opacity file per layer (H2 Rayleigh from ``opacityRayleigh.py`` plus a grey
+    absorption that grows with depth), a Mie cloud opacity file (``opacityMie.py``,
+    restated in ``artes_amd.mie``; constant refractive index 1.5+0.001i, gamma size
+    distribution r_eff 0.5 micron) and an ``atmosphere.in`` that places the cloud in
+    radial layers 4-11, theta cells 1-3 and phi cells 0-2 of a 16 x 6 x 6 grid; then runs
+    ``artes_amd.atmosphere.build`` (``atmosphere.py``), which writes ``atmosphere.fits``.
+
+    The cloud is mixed into the gas by extinction weight (``atmosphere.py:366-369``), so
+    every cloudy layer and wavelength has its own scattering matrix (25 distinct ones):
+    more than the event kernel can stage in LDS, i.e. the per-cell matrix-id path.
+    """
+    from . import gas, mie
+
+    opd = os.path.join(directory, "opacity")
+    os.makedirs(opd, exist_ok=True)
+    wl = [float(w) for w in wavelength]
+    p, t = gas.pt_isothermal(1200.0, 1e-4, p_max, levels)
+    gas.write_pt_file(directory, p, t)
+    op_r, sc_r = op.rayleigh(wl)
+    for i in range(levels - 1):
+        o = op_r.copy()
+        o[2] = o[3] * gas_absorption * (i + 1)
+        o[1] = o[2] + o[3]
+        op.write_opacity_fits(os.path.join(opd, f"gas_opacity_{i + 1:02d}.fits"), o, sc_r)
+    ri = (np.array([0.3, 1.0]), np.array([1.5, 1.5]), np.array([1e-3, 1e-3]))
+    oc, sc = mie.mie_opacity(ri, wl, density=1.0, nr=200, r_eff=0.5, v_eff=0.1)
+    op.write_opacity_fits(os.path.join(opd, "cloud.fits"), oc, sc)
+    with open(os.path.join(directory, "atmosphere.in"), "w") as f:
+        f.write(CLOUDY_IN.format(cloud_density=cloud_density))
+    from . import atmosphere
+
+    return atmosphere.build(directory)
 
 
 def make_thermal(kind: str = "ray", nr: int = 16, ntheta: int = 8, nphi: int = 8, tau_abs: float = 1.0,
