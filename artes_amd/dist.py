@@ -70,11 +70,20 @@ def allreduce_numpy(arrays: list[np.ndarray], world: int) -> list[np.ndarray]:
     import torch
     import torch.distributed as dist
 
-    out = []
+    # RCCL reduces device memory only: under the nccl backend the host arrays travel
+    # through the rank's GPU in ONE flat buffer (one all_reduce per call, as in bench.py)
+    on_gpu = dist.get_backend() == "nccl"
+    flat = np.concatenate([np.ascontiguousarray(a, dtype=np.float64).ravel() for a in arrays])
+    t = torch.from_numpy(flat)
+    if on_gpu:
+        t = t.to(torch.device("cuda", torch.cuda.current_device()))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    flat = t.cpu().numpy() if on_gpu else t.numpy()
+    out, at = [], 0
     for a in arrays:
-        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        out.append(t.numpy().astype(a.dtype, copy=False) if a.dtype != np.float64 else t.numpy())
+        v = flat[at:at + a.size].reshape(a.shape)
+        at += a.size
+        out.append(v.astype(a.dtype) if a.dtype != np.float64 else v.copy())
     return out
 
 
@@ -84,12 +93,12 @@ def run_sharded(transport, n_packets: int, seed: int, r: Rank):
     first, count = shard(n_packets, r.rank, r.world)
     res = transport(first, count, seed)
     if r.world > 1:
-        det, tot, cnt, err = allreduce_numpy([res.det, res.totals, res.counters.astype(np.float64),
-                                              res.err.astype(np.float64)], r.world)
-        res.det, res.totals = det, tot
-        res.counters = np.rint(cnt).astype(np.uint64)
-        res.err = np.rint(err).astype(np.uint64)
-        for k in ("flow_global", "flow_latitudinal"):
-            if getattr(res, k, None) is not None:
-                setattr(res, k, allreduce_numpy([getattr(res, k)], r.world)[0])
+        flows = [k for k in ("flow_global", "flow_latitudinal") if getattr(res, k, None) is not None]
+        red = allreduce_numpy([res.det, res.totals, res.counters.astype(np.float64), res.err.astype(np.float64)]
+                              + [getattr(res, k) for k in flows], r.world)
+        res.det, res.totals = red[0], red[1]
+        res.counters = np.rint(red[2]).astype(np.uint64)
+        res.err = np.rint(red[3]).astype(np.uint64)
+        for k, v in zip(flows, red[4:]):
+            setattr(res, k, v)
     return res
