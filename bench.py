@@ -59,7 +59,10 @@ def main() -> int:
     ap.add_argument("--packets", type=float, default=1e9, help="packets per GPU per step")
     ap.add_argument("--seed", type=int, default=20171015)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the untimed parity step (profiling passes)")
+    ap.add_argument("--no-variants", action="store_true", help="skip the untimed 32^3-grid leg (profiling passes)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"))
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_sq_summary.json"))
     args = ap.parse_args()
 
     import numpy as np
@@ -176,7 +179,7 @@ def main() -> int:
     # same workload, untimed, with the packet-level moments the honest per-pixel errors need
     parity = None
     ref_dir = os.path.join(ROOT, "tests", "golden", "reference_runs", "t_ray3d_ARTES_det_1e6")
-    if os.path.isdir(ref_dir):
+    if os.path.isdir(ref_dir) and not args.no_parity:
         check = driver.run_params(cfg, det_geom, 0, cell_depth=grid.cell_depth(0), packet_moments=True)
         det.zero_(); tot2.zero_()
         grid.run_device(check, 0, per_gpu, args.seed + 1, det.data_ptr(), tot2.data_ptr(), 0, 0, stream.cuda_stream)
@@ -190,6 +193,37 @@ def main() -> int:
                   "pixels": cmp["n_pixels"], "I_total": ph[0] * 1e-6, "I_total_reference": float(ref_ph[1]),
                   "reference": "tests/golden/reference_runs/t_ray3d_ARTES_det_1e6 (1e6 packets)",
                   "sample": f"{per_gpu} packets on rank 0, untimed, packet moments on"}
+
+    # the metric's "32^3 grid": the same workload on 32 x 32 x 32 (r, theta, phi) cells,
+    # one step of the same packet count, rank 0 at N = 1 (the headline value stays configs[2])
+    grid32 = None
+    if world == 1 and not args.no_variants:
+        atm32 = synthetic.make_config("ray3d", ntheta=32, share_matrix=True)
+        g32 = Grid(atm32, device=dev)
+        d32 = driver.detector_geometry(cfg, float(atm32["radial"][-1]))
+        p32 = driver.run_params(cfg, d32, 0, cell_depth=g32.cell_depth(0), packet_moments=False)
+        det.zero_(); tot2.zero_(); cnt.zero_()
+        g32.run_device(p32, 0, 10**7, args.seed, det.data_ptr(), tot2.data_ptr(), 0, 0, stream.cuda_stream)
+        torch.cuda.synchronize()
+        cnt.zero_()
+        t32 = time.perf_counter()
+        g32.run_device(p32, 0, per_gpu, args.seed, det.data_ptr(), tot2.data_ptr(), cnt.data_ptr(), 0, stream.cuda_stream)
+        torch.cuda.synchronize()
+        dt32 = time.perf_counter() - t32
+        c32 = cnt.cpu().numpy().astype(np.float64) / per_gpu
+        grid32 = {"grid": "32x32x32 (r,theta,phi)", "value": round(per_gpu / dt32 / 1e6, 3), "unit": "Mphotons/s",
+                  "packets": per_gpu, "ms": round(dt32 * 1e3, 3),
+                  "events_per_packet": {"crossings": round(c32[0], 3), "scatters": round(c32[1], 4)},
+                  "sample": "one untimed-region step on rank 0, same workload otherwise"}
+        g32.close()
+
+    # what bounds k_trace (committed SQ counter passes, tools/pmc_sq_summary.py)
+    compute = None
+    if os.path.exists(args.sq_json):
+        try:
+            compute = {"source": os.path.relpath(args.sq_json, ROOT), **json.load(open(args.sq_json))["kernels"]}
+        except Exception:
+            compute = None
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -220,6 +254,8 @@ def main() -> int:
                      "events_per_packet": {"crossings": round(C, 3), "scatters": round(S, 4), "peels": round(P, 4)}},
         "cpu_baseline": cpu,
         "parity": parity,
+        "grid_32cubed": grid32,
+        "valu_issue": compute,
         "errors": {str(i): int(e) for i, e in enumerate(err_h) if e},
     }
     print(json.dumps(out), flush=True)
