@@ -136,45 +136,67 @@ __device__ __forceinline__ void family_candidates(const DevGrid& G, const TraceT
     const double rb0 = fast_div(qc0, q0);
     const double ra1 = fast_div(isP ? num1 : q1, isP ? den1 : qa1);
     const double rb1 = fast_div(qc1, q1);
-    // phi rules (ARTES.f90:3311-3346)
-    const bool on_p = (ft == 3);
-    const double sp0 = (!(on_p && fi == cp) && fabs(den0) > 0.0) ? ra0 : 0.0;
-    const double p_in = (sp0 > 1.e-15 && sp0 < 1.e100) ? sp0 : 0.0;
-    const bool okp = !(on_p && fi == pout) && fabs(den1) > 0.0;
-    const double p_out = (okp && ra1 > 1.e-15 && sp0 < 1.e100) ? ra1 : 0.0;   // sic: sp0 (ARTES.f90:3318, 3346)
-    // quadratic roots; 0 where absent (ARTES.f90:4154-4173)
-    const bool ok0 = disc0 >= 0.0, ok1 = disc1 >= 0.0;
-    double s00 = (ok0 && fabs(qa0) > 1.e-100) ? ra0 : 0.0, s01 = (ok0 && fabs(q0) > 1.e-100) ? rb0 : 0.0;
-    double s10 = (ok1 && fabs(qa1) > 1.e-100) ? ra1 : 0.0, s11 = (ok1 && fabs(q1) > 1.e-100) ? rb1 : 0.0;
+    // Per face k (0 inner, 1 outer) the reference's rules reduce to: two roots a_k, b_k
+    // (phi planes and the 90-degree plane: one), each a candidate when it exists, lies
+    // on the right nappe (cones) and exceeds the face's tolerance; the nearer candidate
+    // wins, none if both are equal or the winner is >= 1e100 (quadratic_equation +
+    // cell_face root choice, ARTES.f90:2885-3350, 4154-4173); and a per-face veto
+    // (same-face and grid-edge rules).  Absent candidates are +inf and the choice is
+    // one min, so the wave executes one selection per face instead of one per family
+    // and rule.  The phi and 90-degree-plane rules keep their own cap (none) and
+    // tolerance (0) exactly.
     const int kout = kin + 1;
+    const int kin_f = isP ? cp : kin, kout_f = isP ? pout : kout;
+    const int ftype = isR ? 1 : (isT ? 2 : 3);
+    const bool same0 = (ft == ftype && fi == kin_f), same1 = (ft == ftype && fi == kout_f);
     const int fl0 = T.tfl[isT ? kin : 0], fl1 = T.tfl[isT ? kout : 0];
+    const bool plane0 = isT && !(fl0 & TF_CONE), plane1 = isT && !(fl1 & TF_CONE);
+    // roots and their existence
+    const bool q_ok0 = disc0 >= 0.0, q_ok1 = disc1 >= 0.0;
+    bool va0 = isP ? fabs(den0) > 0.0 : (q_ok0 && fabs(qa0) > 1.e-100);
+    bool vb0 = !isP && q_ok0 && fabs(q0) > 1.e-100;
+    bool va1 = isP ? fabs(den1) > 0.0 : (q_ok1 && fabs(qa1) > 1.e-100);
+    bool vb1 = !isP && q_ok1 && fabs(q1) > 1.e-100;
     // cone nappe filter (ARTES.f90:3040-3064): a root on the other nappe is no crossing
-    const bool g0 = isT && (fl0 & TF_GT90), l0 = isT && (fl0 & TF_LT90);
-    const bool g1 = isT && (fl1 & TF_GT90), l1 = isT && (fl1 & TF_LT90);
-    const double z00 = z + s00 * n2, z01 = z + s01 * n2, z10 = z + s10 * n2, z11 = z + s11 * n2;
+    // (the reference's `s > 1e-15` guard is implied by the tolerance test below)
     if (isT) {
-        auto wrong = [&](double s, int fl) {
-            const double zz = z + s * n2;
-            return s > 1.e-15 && ((zz > 0.0 && (fl & TF_GT90)) || (zz < 0.0 && (fl & TF_LT90)));
-        };
-        if (wrong(s00, fl0)) s00 = 0.0;
-        if (wrong(s01, fl0)) s01 = 0.0;
-        if (wrong(s10, fl1)) s10 = 0.0;
-        if (wrong(s11, fl1)) s11 = 0.0;
+        const bool gt0 = fl0 & TF_GT90, lt0 = fl0 & TF_LT90, gt1 = fl1 & TF_GT90, lt1 = fl1 & TF_LT90;
+        const double za0 = fma(ra0, n2, z), zb0 = fma(rb0, n2, z), za1 = fma(ra1, n2, z), zb1 = fma(rb1, n2, z);
+        va0 = va0 && !((za0 > 0.0 && gt0) || (za0 < 0.0 && lt0));
+        vb0 = vb0 && !((zb0 > 0.0 && gt0) || (zb0 < 0.0 && lt0));
+        va1 = va1 && !((za1 > 0.0 && gt1) || (za1 < 0.0 && lt1));
+        vb1 = vb1 && !((zb1 > 0.0 && gt1) || (zb1 < 0.0 && lt1));
     }
-    const int ftype = isR ? 1 : 2;
-    const bool same0 = (ft == ftype && fi == kin), same1 = (ft == ftype && fi == kout);
-    const double p0 = pick_root(s00, s01, (same0 && isT) ? 1.e-3 : 1.e-15);
-    const double p1 = pick_root(s10, s11, same1 ? 1.e-3 : 1.e-15);
-    // sphere rules: the inner sphere the packet sits on is no candidate
-    const double r_in = same0 ? 0.0 : p0, r_out = p1;
-    // theta rules: cone with the same-face filter, or the 90-degree plane (ARTES.f90:3066-3290)
-    const bool cone0 = fl0 & TF_CONE, cone1 = fl1 & TF_CONE;
-    const double ta = cone0 ? ((!same0 || (fl0 & TF_GT90)) ? p0 : 0.0) : ((!same0 && zp > 0.0 && n2 > 1.e-15) ? zp : 0.0);
-    const double tb = cone1 ? ((!same1 || (fl1 & TF_LT90)) ? p1 : 0.0) : ((!same1 && zp > 0.0 && n2 < -1.e-15) ? zp : 0.0);
-    const double t_in = (ct != 0) ? ta : 0.0, t_out = (kout != G.ntheta) ? tb : 0.0;
-    d_in = isP ? p_in : (isT ? t_in : r_in);
-    d_out = isP ? p_out : (isT ? t_out : r_out);
+    // the 90-degree plane: one root at zp, moving towards it (ARTES.f90:3066-3070, 3116-3118)
+    const double a0 = plane0 ? zp : ra0, a1 = plane1 ? zp : ra1;
+    if (plane0) { va0 = n2 > 1.e-15; vb0 = false; }
+    if (plane1) { va1 = n2 < -1.e-15; vb1 = false; }
+    // tolerances: re-crossing the face the packet sits on needs 1e-3 m (spheres: outer
+    // face only, cones: both; ARTES.f90:2944, 3157), 1e-15 otherwise, 0 for the plane
+    const double tol0 = plane0 ? 0.0 : ((same0 && isT) ? 1.e-3 : 1.e-15);
+    const double tol1 = plane1 ? 0.0 : ((same1 && !isP) ? 1.e-3 : 1.e-15);
+    va0 = va0 && a0 > tol0; vb0 = vb0 && rb0 > tol0;
+    va1 = va1 && a1 > tol1; vb1 = vb1 && rb1 > tol1;
+    // vetoes
+    //   spheres: the inner sphere the packet sits on (ARTES.f90:2899-2960)
+    //   theta:   the grid's polar faces; a cone the packet sits on unless the root lies
+    //            beyond the apex side it faces; the plane it sits on (3014-3290)
+    //   phi:     the half-plane the packet sits on; the outer one also when the inner
+    //            face's root is >= 1e100 (sic: sp0, ARTES.f90:3318, 3346)
+    const bool sp0_big = !(same0) && fabs(den0) > 0.0 && !(ra0 < 1.e100);
+    const bool kill0 = isR ? same0
+                     : isT ? (ct == 0 || (same0 && (plane0 || !(fl0 & TF_GT90))))
+                           : same0;
+    const bool kill1 = isR ? false
+                     : isT ? (kout == G.ntheta || (same1 && (plane1 || !(fl1 & TF_LT90))))
+                           : (same1 || sp0_big);
+    constexpr double INF = __builtin_inf();
+    const double m0 = fmin(va0 ? a0 : INF, vb0 ? rb0 : INF);
+    const double m1 = fmin(va1 ? a1 : INF, vb1 ? rb1 : INF);
+    const bool z0 = kill0 || (va0 && vb0 && a0 == rb0) || !(m0 < 1.e100);
+    const bool z1 = kill1 || (va1 && vb1 && a1 == rb1) || !(m1 < 1.e100);
+    d_in = z0 ? 0.0 : m0;
+    d_out = z1 ? 0.0 : m1;
 }
 
 // Energy-transport diagnostics of a propagation segment (output:flow_global /
