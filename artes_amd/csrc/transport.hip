@@ -485,15 +485,17 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     const char* rf = getenv("ARTES_REFILL");
     // refill a wave once this many of its lanes are idle: a 3D step (one of three face
     // families) costs more than a radial-only one, so idle lanes are worth refilling sooner
-    // (ray3d best at 24, radial-only grids at 28-32)
+    // (ray3d best at 20, radial-only grids at 24, with the static shares below)
     const bool grid3d = (T.ntheta > 1 || T.nphi > 1);
-    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? 24 : 32);
+    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? 20 : 24);
     const char* ef = getenv("ARTES_EMIT_FIRST");
     R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
     const char* bw = getenv("ARTES_BACKWARD");
     R.backward = bw ? (atoi(bw) != 0) : 1;
-    const char* sq = getenv("ARTES_STATIC");   // statically split share of the trace list, in 1/64
-    R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : 32;
+    // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
+    // 3D grids 48, radial-only grids all of it (tools/static_sweep.sh)
+    const char* sq = getenv("ARTES_STATIC");
+    R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : (grid3d ? 48 : 64);
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)
     R.det1 = sin(p->det_theta) * sin(p->det_phi);
     R.det2 = cos(p->det_theta);

@@ -42,6 +42,7 @@ def init(backend: str | None = None) -> Rank:
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29511")
+            backend = backend or os.environ.get("ARTES_DIST_BACKEND")   # gloo: multi-rank rehearsal on one GPU
             if backend is None:
                 import torch
 

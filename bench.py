@@ -73,7 +73,9 @@ def main() -> int:
 
     r = dist.init()
     world = r.world
-    dev = r.local_rank
+    # one GPU per rank; more ranks than devices only in a gloo rehearsal (ARTES_DIST_BACKEND=gloo),
+    # since RCCL refuses two ranks on one device
+    dev = r.local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
     per_gpu = int(args.packets)
 
