@@ -263,6 +263,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     // trace that may follow: 2 x crossings at its start + the first trace's steps + 1
     // (from which the forward walk's step count follows at the interaction).  0 otherwise.
     int kb = 0;
+    int parked = 0;   // 1: waiting for the batched forced first interaction (3: after a cell error)
 
     // a trace starts at the packet position with zero optical depth
     auto start_trace = [&](double d0, double d1, double d2) {
@@ -276,7 +277,55 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         if constexpr (G3D) inz = fast_rcp(nz);
     };
 
+    // The forced first interaction at the end of a first trace (ARTES.f90:658-685): one
+    // exp and one log, ~140 VALU instructions, needed by about one lane in three
+    // wave-steps.  The lane parks instead and the wave runs the block for all parked lanes
+    // together once R.batch of them wait (or few lanes are still stepping).
+    auto first_interaction = [&](bool err) {
+        // one exp and one log for every case: e = 1 outside [1e-6, 50)
+        const double tau_first = tacc;
+        const double xi = rng.uni();
+        const bool mid = tau_first >= 1.e-6 && tau_first < 50.0;
+        const double e = mid ? 1.0 - exp(-tau_first) : 1.0;
+        const double tau = -log(1.0 - xi * e);
+        if (mid) wI *= e;
+        mode = S_PROP;
+        // The propagation that follows walks the first trace's chord again, from its start
+        // to optical depth tau (ARTES.f90:689-720).  When the interaction lies in the
+        // chord's far half it is reached in fewer cells from the far end: walk back from
+        // where the first trace stopped (tx, tft, tfi: set when the lane parked) to optical
+        // depth tau_first - tau.  Same cells in reverse, so the same interaction point up to
+        // rounding; crossing counts are kept as the forward walk's (kb).  Not with the flow
+        // diagnostics (segment order).
+        bool back = false;
+        if constexpr (!FLOW) back = R.backward && mid && !err && tau_first - tau < tau;
+        kb = back ? 2 * ncross + (ncross - kb) + 1 : 0;
+        if (back) {
+            ttgt = fmax(tau_first - tau, 0.0);   // tau rounds to <= tau_first + 1 ulp
+            nx = -nx; ny = -ny; nz = -nz;
+            tacc = 0.0;
+            tpar = 0.0;
+            pending = fam_all;
+            if constexpr (G3D) inz = fast_rcp(nz);
+        } else {
+            ttgt = tau;
+            start_trace(nx, ny, nz);
+        }
+    };
+
     for (;;) {
+        {
+            const unsigned long long pk = __ballot(parked != 0);
+            if (pk) {
+                const int stepping = __popcll(__ballot(have && parked == 0));
+                if (__popcll(pk) >= R.batch || stepping < R.batch_min || cur.exhausted) {
+                    if (parked) {
+                        first_interaction(parked & 2);
+                        parked = 0;
+                    }
+                }
+            }
+        }
         // ---------------------------------------------------------------- refill
         if (!cur.exhausted) {
             const unsigned long long idle = __ballot(!have);
@@ -310,7 +359,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         if (cur.exhausted) { dbg_tsteps++; dbg_tlanes += __popcll(__ballot(have)); }
 #endif
         int end = 0;   // 0: continue, else the slot's new mode
-        if (have) {
+        if (have && !parked) {
             // extinction and albedo of the current cell: issued first so the L2 round trip
             // overlaps the face evaluation (the cell is known before the step)
             const int cell = tcr + G.nr * (tct + G.ntheta * tcp);
@@ -450,37 +499,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
                         end = S_END_DROP;
                     } else {
-                        // one exp and one log for every case: e = 1 outside [1e-6, 50)
-                        const double tau_first = tacc;
-                        const double xi = rng.uni();
-                        const bool mid = tau_first >= 1.e-6 && tau_first < 50.0;
-                        const double e = mid ? 1.0 - exp(-tau_first) : 1.0;
-                        const double tau = -log(1.0 - xi * e);
-                        if (mid) wI *= e;
-                        mode = S_PROP;
-                        // The propagation that follows walks the first trace's chord again, from
-                        // its start to optical depth tau (ARTES.f90:689-720).  When the
-                        // interaction lies in the chord's far half it is reached in fewer cells
-                        // from the far end: walk back from where the first trace stopped to
-                        // optical depth tau_first - tau.  Same cells in reverse, so the same
-                        // interaction point up to rounding; crossing counts are kept as the
-                        // forward walk's (bfix).  Not with the flow diagnostics (segment order).
-                        bool back = false;
-                        if constexpr (!FLOW) back = R.backward && mid && !err && tau_first - tau < tau;
-                        kb = back ? 2 * ncross + (ncross - kb) + 1 : 0;
-                        if (back) {
-                            ttgt = fmax(tau_first - tau, 0.0);   // tau rounds to <= tau_first + 1 ulp
-                            tx += best * nx; ty += best * ny; tz += best * nz;
-                            tft = nft; tfi = nfi;
-                            nx = -nx; ny = -ny; nz = -nz;
-                            tacc = 0.0;
-                            tpar = 0.0;
-                            pending = fam_all;
-                            if constexpr (G3D) inz = fast_rcp(nz);
-                        } else {
-                            ttgt = tau;
-                            start_trace(nx, ny, nz);
-                        }
+                        // the forced first interaction waits (parked, at the chord's far end)
+                        // until enough lanes of the wave need it (see the top of the loop)
+                        tx += best * nx; ty += best * ny; tz += best * nz;
+                        tft = nft; tfi = nfi;
+                        parked = err ? 3 : 1;
                     }
                 }
                 if (end) {   // write the packet state back once
