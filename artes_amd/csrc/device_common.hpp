@@ -32,6 +32,7 @@ struct DevGrid {
     const double* __restrict__ phic;     // [nphi]
     const double* __restrict__ kappa;    // [ncell] (this wavelength)
     const double* __restrict__ albedo;   // [ncell]
+    const double* __restrict__ ka;       // [ncell][2]: extinction, albedo (k_trace: one 16-byte load per step)
     const int* __restrict__ matid;       // [ncell]
     const double* __restrict__ mats;     // [nmat][180][16]
     const double* __restrict__ cums;     // [nmat][181][4]

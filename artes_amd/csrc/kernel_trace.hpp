@@ -363,8 +363,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             // extinction and albedo of the current cell: issued first so the L2 round trip
             // overlaps the face evaluation (the cell is known before the step)
             const int cell = tcr + G.nr * (tct + G.ntheta * tcp);
-            const double k = G.kappa[cell];
-            const double alb = G.albedo[cell];
+            // one 16-byte load at a 32-bit byte offset (ncell < 2^28, checked at grid creation)
+            const double2 kv = *(const double2*)((const char*)G.ka + ((unsigned)cell << 4));
+            const double k = kv.x;
+            const double alb = kv.y;
             // ------------------------------------------- evaluate one face family
             const int fam = G3D ? __builtin_ctz(pending) : 0;
             double din, dout;

@@ -69,7 +69,7 @@ struct artes_grid {
     int device = 0;
     HostTables T;
     double *d_rf2 = nullptr, *d_thetaf = nullptr, *d_tan2 = nullptr, *d_phif = nullptr, *d_phis = nullptr,
-           *d_phic = nullptr, *d_kappa = nullptr, *d_albedo = nullptr, *d_mats = nullptr, *d_cums = nullptr,
+           *d_phic = nullptr, *d_kappa = nullptr, *d_albedo = nullptr, *d_ka = nullptr, *d_mats = nullptr, *d_cums = nullptr,
            *d_sc2 = nullptr, *d_ss2 = nullptr;
     int *d_tplane = nullptr, *d_matid = nullptr;
     double *d_rfront = nullptr, *d_tcos = nullptr;
@@ -167,7 +167,7 @@ int32_t artes_device_count(void) {
 void artes_grid_destroy(artes_grid* g) {
     if (!g) return;
     hipSetDevice(g->device);
-    void* ptrs[] = {g->d_rf2, g->d_thetaf, g->d_tan2, g->d_phif, g->d_phis, g->d_phic, g->d_kappa, g->d_albedo,
+    void* ptrs[] = {g->d_rf2, g->d_thetaf, g->d_tan2, g->d_phif, g->d_phis, g->d_phic, g->d_kappa, g->d_albedo, g->d_ka,
                     g->d_mats, g->d_cums, g->d_sc2, g->d_ss2, g->d_tplane, g->d_matid, g->d_copies, g->d_out,
                     g->d_tot, g->d_cnt, g->d_err, g->d_rec, g->d_rfront, g->d_tcos, g->d_th_cdf, g->d_th_weight,
                     g->d_flow};
@@ -205,6 +205,11 @@ int32_t artes_grid_create(const artes_grid_desc* desc, int32_t device, artes_gri
     HIP_TRY(upload(&g->d_phic, T.phic));
     HIP_TRY(upload(&g->d_kappa, T.kappa));
     HIP_TRY(upload(&g->d_albedo, T.albedo));
+    {
+        std::vector<double> ka(2 * T.kappa.size());
+        for (size_t i = 0; i < T.kappa.size(); i++) { ka[2 * i] = T.kappa[i]; ka[2 * i + 1] = T.albedo[i]; }
+        HIP_TRY(upload(&g->d_ka, ka));
+    }
     HIP_TRY(upload(&g->d_matid, T.matid));
     HIP_TRY(upload(&g->d_mats, T.mats));
     HIP_TRY(upload(&g->d_cums, T.cums));
@@ -471,6 +476,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     G.phif = g->d_phif; G.phis = g->d_phis; G.phic = g->d_phic;
     G.kappa = g->d_kappa + (size_t)p->wl_index * T.ncell;
     G.albedo = g->d_albedo + (size_t)p->wl_index * T.ncell;
+    G.ka = g->d_ka + 2 * (size_t)p->wl_index * T.ncell;
     G.matid = g->d_matid + (size_t)p->wl_index * T.ncell;
     G.mats = g->d_mats; G.cums = g->d_cums; G.sc2 = g->d_sc2; G.ss2 = g->d_ss2;
 
@@ -520,6 +526,8 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     if (n > 0 && use_event_engine()) {
         if (T.nr >= 4096 || T.ntheta >= 1024 || T.nphi >= 1024)
             return fail(-22, "event engine packs cells into 12/10/10 bits: nr < 4096, ntheta < 1024, nphi < 1024");
+        if ((long long)T.ncell >= (1LL << 28))
+            return fail(-22, "event engine addresses the per-cell table with 32-bit byte offsets: ncell < 2^28");
         int32_t rc = g3d ? run_event_engine<true>(g, G, R, rec != nullptr, stream)
                          : run_event_engine<false>(g, G, R, rec != nullptr, stream);
         if (rc) return rc;
