@@ -249,6 +249,8 @@ def main() -> int:
                    "packets_per_gpu_per_step": per_gpu, "parallelism": f"packet-sharded x{world}, RCCL detector all-reduce"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     # measured L2<->fabric bytes of the committed PMC passes over this step's transport time
+                     "traffic_gbs": round(traffic / (k_ms * 1e-3) / 1e9, 2) if traffic else None,
                      "kernel": "transport pipeline per step (k_trace + k_event + k_emit + aux launches)",
                      "kernel_ms": round(k_ms, 3), "step_ms_hip_events": round(float(np.mean(step_ms)), 3),
                      "kernels": kernels,
