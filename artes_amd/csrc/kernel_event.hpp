@@ -610,7 +610,6 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
     double t2[4] = {0, 0, 0, 0};
     double f_emit = 0.0, f_exit = 0.0;   // thermal flux_emitted / flux_exit (ARTES.f90:607, 780, 953)
     const int n_pad = (n + 63) & ~63;
-    const int lane = threadIdx.x & 63;
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
         const int slot = i < n ? L.emit[i] : -1;
         const int m = slot >= 0 ? S.s[slot].mode : S_RETIRED;
