@@ -169,6 +169,14 @@ def main() -> int:
     kernels = {k: {"ms_per_step": round(ms / args.steps, 3), "launches_per_step": round(n / args.steps, 1),
                    "avg_launch_ms": round(ms / n, 4) if n else None}
                for k, (ms, n) in ktimes.items() if n}
+    dominant = None
+    if "trace" in ktimes and ktimes["trace"][1]:
+        t_ms, t_n = ktimes["trace"]
+        per_launch = (B_PER_CROSSING * C + 8.0 * S) * per_gpu * args.steps / t_n
+        dominant = {"name": "k_trace", "alg_bytes_per_packet": round(B_PER_CROSSING * C + 8.0 * S, 1),
+                    "alg_bytes_per_launch": round(per_launch), "avg_launch_ms": round(t_ms / t_n, 4),
+                    "achieved_gbs": round(per_launch / (t_ms / t_n * 1e-3) / 1e9, 2),
+                    "bound": "VALU issue (valu_issue below), not HBM"}
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
@@ -255,6 +263,9 @@ def main() -> int:
                      "kernel_ms": round(k_ms, 3), "step_ms_hip_events": round(float(np.mean(step_ms)), 3),
                      "kernels": kernels,
                      "bytes_per_packet_alg": round(b_alg, 1),
+                     # the dominant kernel alone: its share of B_alg (the kappa gather of every
+                     # crossing and the albedo read at every interaction) over its launches
+                     "dominant_kernel": dominant,
                      "events_per_packet": {"crossings": round(C, 3), "scatters": round(S, 4), "peels": round(P, 4)}},
         "cpu_baseline": cpu,
         "parity": parity,
