@@ -63,6 +63,16 @@ struct alignas(256) Slot {
 static_assert(sizeof(Slot) == 256, "slot record must be two cache lines");
 static_assert(offsetof(Slot, cos_surf) == 128, "line 0 must hold the whole transport state");
 
+// line 0 of a slot as k_event reads it (loaded one event ahead, see k_event)
+struct alignas(16) Line0 {
+    double px, py, pz, dx, dy, dz, ttgt;
+    unsigned long long r0, r1;
+    int pcell, pface, mode, ncross;
+    double wI, tpeel, q1, q2, q3;
+};
+static_assert(sizeof(Line0) == 128 && offsetof(Line0, wI) == offsetof(Slot, wI) && offsetof(Line0, q3) == offsetof(Slot, q3),
+              "Line0 mirrors line 0 of Slot");
+
 struct Pool {
     int P;
     Slot* __restrict__ s;
@@ -323,27 +333,28 @@ __device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S
 // `acc` takes planes 0-8 (I Q U V sums, their squares, the peel count)
 // at plane stride `plane`:
 // the block's LDS detector or the global copy; `det` (global) takes moments 12-15
-__device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
-                                         double* __restrict__ acc, size_t plane, uint32_t& c_scat, uint32_t& c_det) {
+__device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, const Line0& L0,
+                                         double* __restrict__ det, double* __restrict__ acc, size_t plane, uint32_t& c_scat,
+                                         uint32_t& c_det) {
     {
-        const int m = S.s[slot].mode;
+        const int m = L0.mode;
         if ((m & 0xFF) == S_SURF_HIT) return event_surface_hit(G, R, S, slot);
         const int kind = (m >> PEEL_KIND_SHIFT) & 3;
         if (kind == 1) return event_thermal(R, S, slot, det, acc, plane, c_det);
         if (kind == 2) return event_surface_peel(R, S, slot, det, acc, plane, c_det);
         if (m & FLAG_ERR) { S.s[slot].mode = S_END_DROP; return 2; }
-        const double px = S.s[slot].px, py = S.s[slot].py, pz = S.s[slot].pz;
-        double dx = S.s[slot].dx, dy = S.s[slot].dy, dz = S.s[slot].dz;
+        const double px = L0.px, py = L0.py, pz = L0.pz;
+        double dx = L0.dx, dy = L0.dy, dz = L0.dz;
         // k_trace scaled I by the forced-first-interaction and albedo weights (ARTES.f90:
         // 674-676, 801-807); the polarised components follow by the same factor
-        const double wI = S.s[slot].wI;
-        double st[4] = {wI, S.s[slot].q1 * wI, S.s[slot].q2 * wI, S.s[slot].q3 * wI};
+        const double wI = L0.wI;
+        double st[4] = {wI, L0.q1 * wI, L0.q2 * wI, L0.q3 * wI};
         int cr, ct, cp;
-        unpack_cell(S.s[slot].pcell, cr, ct, cp);
+        unpack_cell(L0.pcell, cr, ct, cp);
         const int cell = cr + G.nr * (ct + G.ntheta * cp);
         const int mid = G.nmat == 1 ? 0 : G.matid[cell];   // uniform atmosphere: no dependent load
         const double* __restrict__ P = G.mats + (size_t)mid * MAT_DOUBLES;
-        const double tau_peel = S.s[slot].tpeel;
+        const double tau_peel = L0.tpeel;
         bool drop = false;
         if ((m & FLAG_EXIT) && tau_peel < 50.0) {
             const double w = exp(-tau_peel);
@@ -423,7 +434,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         // scatter_photon + polarization_rotation (ARTES.f90:819-846)
         c_scat++;
         if (R.rec) S.s[slot].nscat += 1;
-        Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
+        Rng rng; rng.s0 = L0.r0; rng.s1 = L0.r1;
         double alpha, beta;
         sample_angles(G, R, G.cums + (size_t)mid * CUM_DOUBLES, rng, st, alpha, beta);
         double e0, e1, e2;
@@ -495,13 +506,27 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
     const int n = *L.event_n;
     uint32_t c_scat = 0, c_det = 0;
     const int n_pad = (n + 63) & ~63;   // whole waves iterate together (wave-aggregated appends)
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
-        const int slot = i < n ? L.event[i] : -1;
-        const int dest = slot >= 0 ? event_one(G, R, S, slot, det, acc, plane, c_scat, c_det) : 0;
+    // Software pipeline: the slot ids come two events ahead and line 0 of the next event's
+    // record one event ahead, so the record loads (random lines in the pool) overlap the
+    // current event's arithmetic instead of stalling at its start.
+    const int stride = (int)gridDim.x * BLOCK;
+    int i = blockIdx.x * BLOCK + threadIdx.x;
+    int slot = i < n ? L.event[i] : -1;
+    int slot_n = i + stride < n ? L.event[i + stride] : -1;
+    Line0 cur;
+    if (slot >= 0) cur = *(const Line0*)(S.s + slot);
+    for (; i < n_pad; i += stride) {
+        const int slot_nn = i + 2 * stride < n ? L.event[i + 2 * stride] : -1;
+        Line0 nxt;
+        if (slot_n >= 0) nxt = *(const Line0*)(S.s + slot_n);
+        const int dest = slot >= 0 ? event_one(G, R, S, slot, cur, det, acc, plane, c_scat, c_det) : 0;
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
         if (i < n) L.trace_out[R.emit_first ? S.P - 1 - i : i] = (dest == 1) ? slot : -1;
         wave_append(dest == 2, slot, L.emit, L.emit_n);
+        slot = slot_n;
+        slot_n = slot_nn;
+        cur = nxt;
     }
     if constexpr (LDS_D) {
         __syncthreads();
