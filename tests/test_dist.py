@@ -21,7 +21,7 @@ from artes_amd import dist, driver, synthetic
 from artes_amd.engine import RunResult
 from oracle.oracle import OracleGrid
 
-r = dist.init(backend="gloo")
+r = dist.init()   # backend from ARTES_DIST_BACKEND (the one-GPU rehearsal's switch)
 atm = synthetic.make_config("ray3d", nr=6, ntheta=4, nphi=6)
 cfg = driver.default_config()
 det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
@@ -34,6 +34,7 @@ def transport(first, n, seed):
 
 res = dist.run_sharded(transport, 30001, 99, r)
 if r.rank == 0:
+    open({out!r}.replace("det2.npy", "backend.txt"), "w").write(tdist.get_backend())
     np.save({out!r}, res.det)
     np.save({out!r}.replace(".npy", "_cnt.npy"), res.counters)
     np.save({out!r}.replace(".npy", "_flow.npy"), res.flow_global)
@@ -55,11 +56,12 @@ def test_two_rank_gloo_equals_single_process(tmp_path):
     out = str(tmp_path / "det2.npy")
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(root=ROOT, out=out))
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29633", WORLD_SIZE="2")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29633", WORLD_SIZE="2", ARTES_DIST_BACKEND="gloo")
     procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(k), LOCAL_RANK=str(k)))
              for k in range(2)]
     for pr in procs:
         assert pr.wait(timeout=300) == 0
+    assert open(str(tmp_path / "backend.txt")).read() == "gloo"
     det2 = np.load(out)
     cnt2 = np.load(out.replace(".npy", "_cnt.npy"))
 
