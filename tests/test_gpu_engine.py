@@ -142,3 +142,29 @@ def test_zero_and_tiny_runs(require_gpu):
     assert r1.counter("packets") == 1
     r7 = grid.run(p, 5, 7, 1)
     assert r7.counter("packets") == 7
+
+
+def test_bench_line_contract(require_gpu):
+    """bench.py (the driver's measurement) prints one JSON line with the contract's fields,
+    on a small packet count (a subprocess: the bench owns its process)."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--packets", "2e6", "--steps", "2", "--warmup", "1",
+                          "--no-cpu-baseline", "--no-variants", "--no-parity"],
+                         capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-4
+    assert r["events_per_packet"]["crossings"] > 50 and d["errors"] == {}
