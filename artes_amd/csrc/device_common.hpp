@@ -64,7 +64,7 @@ struct DevRun {
     double* __restrict__ tot2;      // [6] packet-level sum T^2 per Stokes, flux_emitted, flux_exit
     unsigned long long* __restrict__ cnt;   // [ARTES_NUM_COUNTERS]
     unsigned long long* __restrict__ err;   // [ARTES_NUM_ERR]
-    double* __restrict__ rec;       // [n][4] (TRACE builds)
+    double* __restrict__ rec;       // [n][ARTES_TRACE_FIELDS] (TRACE builds)
     double* __restrict__ flow_g;    // [ncell][3] flow_global accumulators, or null
     double* __restrict__ flow_t;    // [ncell][4] flow_latitudinal accumulators, or null
 };

@@ -5,7 +5,7 @@
 // execute the union of all lanes' branches, and carrying the whole packet state plus
 // the scattering math in one kernel costs ~300 VGPRs (one wave per SIMD).  Here the
 // packet life is split at its natural seams into three kernels over a pool of P
-// in-flight packets whose state lives in HBM (SoA, ~250 B/packet):
+// in-flight packets whose state lives in HBM (one 256-byte record per packet, `Slot`):
 //
 //   k_trace  the hot loop: cell_face steps (ARTES.f90:2800-3470) of every trace --
 //            first optical depth (625-656), propagation (689-778, 848-941) and peel-off
@@ -58,7 +58,8 @@ struct alignas(256) Slot {
     double peel_sum;                    // trace records: total peeled intensity
     unsigned long long pid;             // trace records: packet id
     int cur_pix, nscat;                 // moments: current pixel; trace records: scatterings
-    double spare1[4];
+    double peel_pol[3];                 // trace records: peeled -Q, U, V (detector sign, ARTES.f90:4956)
+    double spare1;
 };
 static_assert(sizeof(Slot) == 256, "slot record must be two cache lines");
 static_assert(offsetof(Slot, cos_surf) == 128, "line 0 must hold the whole transport state");
@@ -422,7 +423,10 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                             S.s[slot].cs2 = cs[2] + v[2]; S.s[slot].cs3 = cs[3] + v[3];
                             S.s[slot].pt0 += v[0]; S.s[slot].pt1 += v[1]; S.s[slot].pt2 += v[2]; S.s[slot].pt3 += v[3];
                         }
-                        if (R.rec) S.s[slot].peel_sum += wI;
+                        if (R.rec) {
+                            S.s[slot].peel_sum += wI;
+                            S.s[slot].peel_pol[0] += v[1]; S.s[slot].peel_pol[1] += v[2]; S.s[slot].peel_pol[2] += v[3];
+                        }
                         c_det++;
                     }
                 } else {
@@ -655,11 +659,15 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
             }
             if (m == S_END_EXIT && R.photon_source == 2) f_exit += S.s[slot].wI;
             if constexpr (TRACE) {
-                double* rr = R.rec + (size_t)(S.s[slot].pid - R.first) * 4;
+                double* rr = R.rec + (size_t)(S.s[slot].pid - R.first) * ARTES_TRACE_FIELDS;
                 rr[0] = S.s[slot].peel_sum;
                 rr[1] = (double)S.s[slot].nscat;
                 rr[2] = (double)S.s[slot].ncross;
                 rr[3] = (double)(m - S_END_EXIT + 1);   // 1 exit, 2 absorbed, 3 dropped
+                rr[4] = S.s[slot].peel_pol[0];
+                rr[5] = S.s[slot].peel_pol[1];
+                rr[6] = S.s[slot].peel_pol[2];
+                rr[7] = 0.0;
             }
         }
         const unsigned long long k = pkt0 + (unsigned long long)i;
@@ -735,6 +743,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         if constexpr (TRACE) {
             S.s[slot].pid = pid;
             S.s[slot].peel_sum = 0.0;
+            S.s[slot].peel_pol[0] = S.s[slot].peel_pol[1] = S.s[slot].peel_pol[2] = 0.0;
             S.s[slot].nscat = 0;
         }
         }   // emit

@@ -216,16 +216,17 @@ __global__ __launch_bounds__(BLOCK) void transport_kernel(DevGrid G, DevRun R) {
                     for (int k = 0; k < 4; k++) { unsafeAtomicAdd(&det[(12 + k) * plane + cur], s_cs[k][lane] * s_cs[k][lane]); s_cs[k][lane] = 0.0; }
                     s_pix[lane] = -1;
                 }
+                if constexpr (TRACE) {   // s_pt holds the packet's peeled I, -Q, U, V totals
+                    double* rr = R.rec + (size_t)(pid - R.first) * ARTES_TRACE_FIELDS;
+                    rr[0] = rec_peel; rr[1] = (double)rec_scat; rr[2] = (double)rec_cross; rr[3] = (double)endst;
+                    rr[4] = s_pt[1][lane]; rr[5] = s_pt[2][lane]; rr[6] = s_pt[3][lane]; rr[7] = 0.0;
+                    rec_peel = 0.0; rec_scat = 0; rec_cross = 0;
+                }
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const double t = s_pt[k][lane];
                     if (t != 0.0) atomicAdd(&s_tot2[k], t * t);
                     s_pt[k][lane] = 0.0;
-                }
-                if constexpr (TRACE) {
-                    double* rr = R.rec + (size_t)(pid - R.first) * 4;
-                    rr[0] = rec_peel; rr[1] = (double)rec_scat; rr[2] = (double)rec_cross; rr[3] = (double)endst;
-                    rec_peel = 0.0; rec_scat = 0; rec_cross = 0;
                 }
                 have_pkt = false;
             }

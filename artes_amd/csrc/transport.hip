@@ -1,22 +1,23 @@
 // transport.hip -- MI355X (gfx950) photon-packet transport engine + C ABI.
 //
-// The hot path of the reference, `radiative_transfer` (ARTES.f90:518-1006), runs here
-// as ONE persistent HIP kernel: one packet per lane, 64-lane waves, each lane
-// refilling itself with the next packet of its static interleaved share as soon as
-// its packet ends.  A packet's life is a state machine whose dominant state is a
-// single uniform "trace step" (one cell_face call, ARTES.f90:2800-3470), shared by
-// the three traces of the reference -- first optical depth (625-656), propagation
-// (689-778 / 848-941) and peel-off (4739-4761) -- so the branchy geometry runs
-// converged across the wave.  The rare, expensive event (peel contribution +
-// scattering, ~2.5 per packet vs ~110 trace steps) is deferred until enough lanes of
-// the wave need it (`R.defer`), so it runs with many lanes active instead of
-// executing almost every iteration with one or two.
+// The hot path of the reference, `radiative_transfer` (ARTES.f90:518-1006), runs here as
+// an EVENT ENGINE over a pool of in-flight packets in HBM (one 256-byte record per slot,
+// kernel_event.hpp): one host iteration launches
+//   k_trace  (kernel_trace.hpp) every cell_face step (ARTES.f90:2800-3470) of the first
+//            optical depth, propagation and peel-off traces, one packet per lane, lanes
+//            refilling themselves from the trace list;
+//   k_event  peel-off contribution + scattering (ARTES.f90:4765-4984, 819-846);
+//   k_emit   packet close-out + emission of new packets (ARTES.f90:546-597, 1027-1268);
+//   k_rotate list rotation;
+// and the host polls the live-packet count every few iterations until the pool drains.
+// The fused single-kernel engine of the first design (kernel_persistent.hpp) is kept as
+// ARTES_ENGINE=persistent for comparison tests only.
 //
-// All arithmetic is FP64 (the reference is double precision; the cell-face
-// quadratics cancel ~15 digits at R ~ 7e7 m).  Tables: see tables.hpp.
-// Detector: FP64 atomics into NCOPY privatised copies (copy = blockIdx % NCOPY, i.e.
-// one per XCD under round-robin dispatch -- a speed heuristic only), summed by a
-// small reduce kernel.  No MFMA: this is branchy per-packet work, not a contraction.
+// All arithmetic is FP64 (the reference is double precision; the cell-face quadratics
+// cancel ~15 digits at R ~ 7e7 m).  Tables: tables.hpp.  Detector: planes
+// 0-8 accumulated per k_event block in LDS and flushed into NCOPY privatised HBM copies
+// (copy = blockIdx % NCOPY), summed by reduce_detector.  No MFMA: this is branchy
+// per-packet work, not a contraction.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -102,12 +103,28 @@ struct artes_grid {
     hipEvent_t ev_poll = nullptr;
     int trace_blocks = 0;
     long long last_iterations = 0;
+    // occupancy answers per (kernel, dynamic LDS bytes), queried once per grid
+    std::vector<std::pair<std::pair<const void*, size_t>, int>> occ;
     // per-launch timing (artes_set_profiling)
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;     // start/end pairs
     std::vector<int> prof_kind;
     size_t prof_used = 0;
 };
+
+// resident blocks per CU of `kernel` at `lds` bytes of dynamic LDS (cached per grid: the
+// event engine launches the same few kernels hundreds of times per call)
+template <class K>
+static int blocks_per_cu(artes_grid* g, K kernel, size_t lds) {
+    const std::pair<const void*, size_t> key{(const void*)kernel, lds};
+    for (const auto& e : g->occ)
+        if (e.first == key) return e.second;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BLOCK, lds) != hipSuccess) per_cu = 1;
+    per_cu = std::max(1, per_cu);
+    g->occ.push_back({key, per_cu});
+    return per_cu;
+}
 
 // run `launch` between two recorded events when profiling is on
 template <class F>
@@ -263,7 +280,7 @@ static bool use_event_engine() {
     return !(e && std::string(e) == "persistent");
 }
 
-// allocate the packet pool (SoA) and the work lists of the event engine
+// allocate the packet pool (256-byte slot records) and the work lists of the event engine
 static int32_t ensure_pool(artes_grid* g) {
     if (g->pool_mem) return 0;
     const char* env = getenv("ARTES_POOL");
@@ -290,13 +307,10 @@ static int32_t ensure_pool(artes_grid* g) {
 
 // k_trace (kernel_trace.hpp) with its face tables in LDS
 template <bool G3D, bool OBL, int WPE, bool FLOW = false>
-static void launch_trace(artes_grid* g, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
+static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
     const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
-    int per_cu = 0;
-    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<G3D, OBL, WPE, FLOW>, BLOCK, lds);
-    const char* bp = getenv("ARTES_TRACE_BPC");   // blocks per CU override (tuning)
-    if (bp) per_cu = atoi(bp);
-    g->trace_blocks = std::max(1, per_cu) * g->num_cus;
+    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW>, lds);
+    g->trace_blocks = per_cu * g->num_cus;
     timed(g, ARTES_K_TRACE, stream, [&] {
         hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
@@ -305,17 +319,18 @@ static void launch_trace(artes_grid* g, const DevGrid& G, const DevRun& R, const
 // k_trace variant: 3D or radial-only grid, spheroidal (oblate) or spherical planet,
 // occupancy target (waves per SIMD the register budget is sized for)
 template <bool G3D>
-static void launch_trace_any(artes_grid* g, int wpe, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
+static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, const DevRun& R, const Lists& L,
+                             hipStream_t stream) {
     const bool oblate = !(G.ax2 == 1.0 && G.by2 == 1.0 && G.cz2 == 1.0 && G.a == 1.0 && G.b == 1.0);
     if (R.flow_g || R.flow_t) {   // diagnostics: one occupancy target only
-        if (oblate) launch_trace<G3D, true, 4, true>(g, G, R, L, stream);
-        else launch_trace<G3D, false, 4, true>(g, G, R, L, stream);
+        if (oblate) launch_trace<G3D, true, 4, true>(g, bpc, G, R, L, stream);
+        else launch_trace<G3D, false, 4, true>(g, bpc, G, R, L, stream);
     } else if (oblate) {
-        if (wpe == 3) launch_trace<G3D, true, 3>(g, G, R, L, stream);
-        else launch_trace<G3D, true, 4>(g, G, R, L, stream);
+        if (wpe == 3) launch_trace<G3D, true, 3>(g, bpc, G, R, L, stream);
+        else launch_trace<G3D, true, 4>(g, bpc, G, R, L, stream);
     } else {
-        if (wpe == 3) launch_trace<G3D, false, 3>(g, G, R, L, stream);
-        else launch_trace<G3D, false, 4>(g, G, R, L, stream);
+        if (wpe == 3) launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
+        else launch_trace<G3D, false, 4>(g, bpc, G, R, L, stream);
     }
 }
 
@@ -329,8 +344,11 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     HIP_TRY(hipMemsetAsync(g->d_next, 0, sizeof(unsigned long long), stream));
     int* cnt = g->d_counts;
     const int side_blocks = std::max(1, g->num_cus * 8);
+    // launch knobs, read once per call (tuning overrides; the defaults are the measured optima)
     const char* we = getenv("ARTES_WPE");
     const int wpe = we ? atoi(we) : 4;
+    const char* bp = getenv("ARTES_TRACE_BPC");   // k_trace blocks per CU
+    const int trace_bpc = bp ? std::max(1, atoi(bp)) : 0;
     if (trace_table_bytes(G.nr, G.ntheta, G.nphi) > 65536) return fail(-22, "face tables exceed the 64 KiB LDS budget of k_trace");
     // scattering tables in LDS for k_event when they fit next to one another (a few
     // distinct matrices: uniform and layered atmospheres); otherwise read from L2
@@ -345,13 +363,11 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const bool det_lds = (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
     int ev_blocks = side_blocks;
     if (det_lds) {
-        int per_cu = 0;
         const size_t b = (ev_lds ? ev_bytes : 0) + det_bytes;
-        if (ev_lds) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_event<true, true>, BLOCK, b);
-        else hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_event<false, true>, BLOCK, b);
+        int per_cu = ev_lds ? blocks_per_cu(g, k_event<true, true>, b) : blocks_per_cu(g, k_event<false, true>, b);
         const char* eb = getenv("ARTES_EVENT_BPC");
-        if (eb) per_cu = atoi(eb);
-        ev_blocks = std::max(1, per_cu) * g->num_cus;
+        if (eb) per_cu = std::max(1, atoi(eb));
+        ev_blocks = per_cu * g->num_cus;
     }
     auto lists = [&](int in) {
         Lists L;
@@ -386,7 +402,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const long long max_it = 2000000LL;
     for (;;) {
         Lists L = lists(in);
-        launch_trace_any<G3D>(g, wpe, G, R, L, stream);
+        launch_trace_any<G3D>(g, wpe, trace_bpc, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
             if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds) hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
@@ -603,13 +619,14 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
         g->out_cap = stride;
     }
     if (records) {
-        if (g->rec_cap < n * 4) {
+        const size_t rec_n = std::max<uint64_t>(n, 1) * ARTES_TRACE_FIELDS;
+        if (g->rec_cap < rec_n) {
             if (g->d_rec) hipFree(g->d_rec);
             g->d_rec = nullptr;
-            HIP_TRY(hipMalloc((void**)&g->d_rec, std::max<uint64_t>(n, 1) * 4 * sizeof(double)));
-            g->rec_cap = n * 4;
+            HIP_TRY(hipMalloc((void**)&g->d_rec, rec_n * sizeof(double)));
+            g->rec_cap = rec_n;
         }
-        HIP_TRY(hipMemset(g->d_rec, 0, std::max<uint64_t>(n, 1) * 4 * sizeof(double)));
+        HIP_TRY(hipMemset(g->d_rec, 0, rec_n * sizeof(double)));
     }
     HIP_TRY(hipMemset(g->d_out, 0, stride * sizeof(double)));
     HIP_TRY(hipMemset(g->d_tot, 0, 6 * sizeof(double)));
@@ -650,7 +667,7 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
         HIP_TRY(hipMemcpy(e, g->d_err, sizeof(e), hipMemcpyDeviceToHost));
         for (int i = 0; i < ARTES_NUM_ERR; i++) err[i] += e[i];
     }
-    if (records) HIP_TRY(hipMemcpy(records, g->d_rec, n * 4 * sizeof(double), hipMemcpyDeviceToHost));
+    if (records) HIP_TRY(hipMemcpy(records, g->d_rec, n * ARTES_TRACE_FIELDS * sizeof(double), hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -669,7 +686,7 @@ int32_t artes_run_flow(artes_grid* g, const artes_run_params* p, uint64_t first,
 
 int32_t artes_run_trace(artes_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
                         double* records) {
-    if (!records) return fail(-22, "null records");
+    if (!g || !p || !records) return fail(-22, "null argument");
     if (n > (1ull << 24)) return fail(-22, "trace runs are limited to 2^24 packets");
     std::vector<double> det((size_t)16 * p->nx * p->ny, 0.0);
     return run_host(g, p, first, n, seed, det.data(), nullptr, nullptr, nullptr, records);

@@ -88,6 +88,17 @@ def allreduce_numpy(arrays: list[np.ndarray], world: int) -> list[np.ndarray]:
     return out
 
 
+def broadcast_int(value: int, r: Rank) -> int:
+    """Rank 0's non-negative ``value`` (< 2^64) on every rank: the clock seed of a CLI run
+    must be the same on every shard, or the global packet ids would not map to one RNG
+    stream set (the result would then depend on the rank start times)."""
+    if r.world <= 1:
+        return int(value)
+    parts = np.array([value >> 32, value & 0xFFFFFFFF], dtype=np.float64) if r.rank == 0 else np.zeros(2)
+    (out,) = allreduce_numpy([parts], r.world)   # exact: each half < 2^32
+    return (int(out[0]) << 32) | int(out[1])
+
+
 def run_sharded(transport, n_packets: int, seed: int, r: Rank):
     """Run ``transport(first, count, seed) -> RunResult`` on this rank's shard and sum
     the results over all ranks (host tensors; the GPU bench uses device tensors + RCCL)."""

@@ -12,8 +12,8 @@ import os
 
 import numpy as np
 
-from .abi import (ARTES_ABI_VERSION, ARTES_NUM_COUNTERS, ARTES_NUM_ERR, ARTES_NUM_TOTALS, COUNTER_NAMES, GridArrays,
-                  GridDesc, RunParams)
+from .abi import (ARTES_ABI_VERSION, ARTES_NUM_COUNTERS, ARTES_NUM_ERR, ARTES_NUM_TOTALS, ARTES_TRACE_FIELDS, COUNTER_NAMES,
+                  GridArrays, GridDesc, RunParams)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ARTES_LIB_PATH") or os.path.join(HERE, "lib", "libartes_hip.so")
@@ -196,7 +196,9 @@ class Grid:
                "artes_run_device_flow")
 
     def trace(self, params: RunParams, first: int, n: int, seed: int) -> np.ndarray:
-        rec = np.zeros((n, 4))
+        """Per-packet records ``[n][ARTES_TRACE_FIELDS]`` (``artes_run_trace``): peeled I, scatterings,
+        crossings, end state (1 exit, 2 absorbed, 3 dropped), peeled -Q, U, V, 0."""
+        rec = np.zeros((n, ARTES_TRACE_FIELDS))
         _check(lib().artes_run_trace(self.h, C.byref(params), int(first), int(n), int(seed),
                                      rec.ctypes.data_as(C.POINTER(C.c_double))), "artes_run_trace")
         return rec

@@ -131,8 +131,8 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
     r_top = float(atm["radial"][-1])
     ntheta = atm["theta"].size - 1
     det = driver.detector_geometry(cfg, r_top)
-    if seed is None:
-        seed = int(time.time() * 1e6) & 0x7FFFFFFFFFFFFFFF
+    if seed is None:   # the reference's clock seed (ARTES.f90:4187), drawn once on rank 0
+        seed = dist.broadcast_int(int(time.time() * 1e6) & 0x7FFFFFFFFFFFFFFF, r)
     if transport_factory is None:
         transport = Transport(atm, device=r.local_rank, oblateness=cfg.oblateness)
     else:
@@ -212,20 +212,27 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
                 write_source(wl, res, False)
                 driver.write_cell_depth(out_dir, wavelengths[wl], source(wl)[0])
     elif mode == "imaging_broad":                         # ARTES.f90:168-204
+        # detector_thread is zeroed once (array_start at wl_count == 1, ARTES.f90:175-180) and
+        # accumulates over the wavelengths; every radiative_transfer call rescales the running
+        # sums by the CURRENT wavelength's package energy (959-975), so the last one wins, and
+        # write_output runs once after the loop (199)
         acc = None
         E = 0.0
         for wl in range(wavelengths.size):
             res = transport_call(wl, det.det_phi)
             err_total += res.err
             acc = res.det[:3].copy() if acc is None else acc + res.det[:3]
-            # every call rescales the running thread sums by the CURRENT wavelength's
-            # package energy (ARTES.f90:959-975 inside the loop): the last one wins
             E = energy(wl, det.det_phi)
+            # planet source: the reference's single write_output reads flux_emitted / flux_exit
+            # after grid_finished(1) has deallocated them (2557-2565, undefined behaviour);
+            # here luminosity.dat gets one line per wavelength instead
             if r.rank == 0 and planet:
                 write_source(wl, res, False)
         if r.rank == 0:
             d = driver.scale_detector(acc, E)
             driver.write_stokes_outputs(out_dir, d, det.pixel_scale)
+            if not planet:   # normalization.dat of the last wavelength (write_output, 3622-3652)
+                write_source(wavelengths.size - 1, None, False)
     elif mode == "phase":                                 # ARTES.f90:206-250
         wl = 0
         for k, phi in enumerate(driver.phase_angles()):

@@ -87,3 +87,15 @@ def compare_to_reference(raw: np.ndarray, n_packets: int, energy: float, pixel_s
                 median_abs_z=float(np.median(np.abs(z))) if z.size else float("nan"),
                 frac_gt4=float(np.mean(np.abs(z) > 4.0)) if z.size else float("nan"),
                 max_abs_z=float(np.max(np.abs(z))) if z.size else float("nan"), n_pixels=int(z.size))
+
+
+def records_agree(a: np.ndarray, b: np.ndarray, rtol: float = 1e-9) -> np.ndarray:
+    """Per-packet agreement of two ``artes_run_trace`` record arrays ``[n][8]`` (GPU engine vs
+    CPU oracle, same seeds): the same scatter count, crossing count and end state, the same
+    peeled Stokes I to ``rtol``, and the same peeled -Q, U, V to ``rtol`` of the peeled I."""
+    scale = np.abs(a[:, 0]) + np.abs(b[:, 0])
+    ok = (np.isclose(a[:, 0], b[:, 0], rtol=rtol, atol=1e-300) & (a[:, 1] == b[:, 1]) & (a[:, 2] == b[:, 2])
+          & (a[:, 3] == b[:, 3]))
+    for k in (4, 5, 6):
+        ok &= np.abs(a[:, k] - b[:, k]) <= rtol * scale + 1e-300
+    return ok

@@ -51,6 +51,15 @@ def cpu_baseline(atm, params, budget_s: float = 15.0) -> dict:
             "sample": f"{n} packets of the same ray3d workload (oracle/artes_oracle.c, {threads} OpenMP threads, {dt:.1f} s)"}
 
 
+def _md5(path: str) -> str | None:
+    import hashlib
+
+    try:
+        return hashlib.md5(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,8 +70,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the untimed parity step (profiling passes)")
     ap.add_argument("--no-variants", action="store_true", help="skip the untimed 32^3-grid leg (profiling passes)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_summary.json"))
-    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_sq_summary.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"))
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_sq_summary.json"))
     args = ap.parse_args()
 
     import numpy as np
@@ -91,37 +100,54 @@ def main() -> int:
     ny, nx = det_geom.ny, det_geom.nx
 
     f64 = dict(dtype=torch.float64, device=f"cuda:{dev}")
-    det = torch.zeros((4, 4, ny, nx), **f64)
-    tot2 = torch.zeros(6, **f64)   # sum T^2 per Stokes, flux_emitted, flux_exit (include/artes_amd.h)
+    # one flat float64 buffer holds everything the ranks exchange, so a step issues ONE sum
+    # all_reduce: the detector [4][4][ny][nx], sum T^2 per Stokes + the two
+    # thermal fluxes (include/artes_amd.h), the counters and the error-code counts (the
+    # engine writes those as uint64 into the int64 tensors; they are converted to float64,
+    # exact below 2^53, before the reduce)
+    n_det = 16 * ny * nx
+    flat = torch.zeros(n_det + 6 + 8 + 64, **f64)
+    det = flat[:n_det].view(4, 4, ny, nx)
+    tot2 = flat[n_det:n_det + 6]
     cnt = torch.zeros(8, dtype=torch.int64, device=f"cuda:{dev}")
     err = torch.zeros(64, dtype=torch.int64, device=f"cuda:{dev}")
     stream = torch.cuda.current_stream()
+    backend = None
+    if world > 1:
+        import torch.distributed as tdist
+
+        backend = tdist.get_backend()
 
     def step(k: int):
-        det.zero_(); tot2.zero_(); cnt.zero_(); err.zero_()
+        flat.zero_(); cnt.zero_(); err.zero_()
         first = (k * world + r.rank) * per_gpu
         grid.run_device(params, first, per_gpu, args.seed, det.data_ptr(), tot2.data_ptr(), cnt.data_ptr(),
                         err.data_ptr(), stream.cuda_stream)
         if world > 1:
-            import torch.distributed as tdist
+            flat[n_det + 6:n_det + 14].copy_(cnt)
+            flat[n_det + 14:].copy_(err)
+            tdist.all_reduce(flat)
 
-            tdist.all_reduce(det)
-            tdist.all_reduce(tot2)
-            tdist.all_reduce(cnt)
-            tdist.all_reduce(err)
+    def counts():
+        """(counters, error codes) of the last step, summed over ranks."""
+        if world > 1:
+            return (flat[n_det + 6:n_det + 14].cpu().numpy().astype(np.float64),
+                    np.rint(flat[n_det + 14:].cpu().numpy()).astype(np.int64))
+        return cnt.cpu().numpy().astype(np.float64), err.cpu().numpy()
 
     def barrier():
         torch.cuda.synchronize()
         if world > 1:
-            import torch.distributed as tdist
-
             tdist.barrier()
         torch.cuda.synchronize()
 
+    # warmup; the last warmup step runs with the per-launch HIP events on, so the timed
+    # region records events that already exist (no hipEventCreate inside it)
     for k in range(args.warmup):
+        grid.set_profiling(k == args.warmup - 1)
         step(k)
     barrier()
-    grid.kernel_times()
+    grid.kernel_times()            # drop the warmup's launches
     grid.set_profiling(True)       # HIP events around every transport launch (per-kernel durations)
     ev = []
     t0 = time.perf_counter()
@@ -129,61 +155,68 @@ def main() -> int:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        step(args.warmup + k)          # the transport kernel runs on `stream`; all_reduce follows
+        step(args.warmup + k)          # the transport kernels run on `stream`; the all_reduce follows
         e1.record(stream)
         ev.append((e0, e1))
     barrier()
     elapsed = time.perf_counter() - t0
-    # transport duration per launch, HIP events on the launch stream, over the timed region
-    # (the step's events bracket run_device and the RCCL reduce; the library's own events
-    # bracket the transport kernel alone for the last launch)
+    # step durations (HIP events on the launch stream: run_device + the RCCL reduce) and the
+    # per-kernel launch durations (the library's events, same stream) over the timed region
     step_ms = [a.elapsed_time(b) for a, b in ev]
     ktimes = grid.kernel_times()   # {class: (summed ms over the timed steps, launches)}
     grid.set_profiling(False)
     if world > 1:
-        import torch.distributed as tdist
-
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
+    cnt_h, err_h = counts()
     if r.rank != 0:
         if world > 1:
-            import torch.distributed as tdist
-
             tdist.barrier()
         return 0
 
     total_packets = per_gpu * world * args.steps
     value = total_packets / elapsed / 1e6
-    cnt_h = cnt.cpu().numpy().astype(np.float64)
-    err_h = err.cpu().numpy()
     n_step = per_gpu * world
     C = cnt_h[0] / n_step
     S = cnt_h[1] / n_step
     P = cnt_h[2] / n_step
     b_alg = B_PER_CROSSING * C + B_PER_SCATTER * S + B_PER_PEEL * P
-    # the transport of one step is a pipeline of launches (k_trace / k_event / k_emit per
-    # iteration); its duration is the sum of their HIP-event durations
-    k_ms = sum(ms for ms, _ in ktimes.values()) / args.steps
-    achieved = b_alg * per_gpu / (k_ms * 1e-3) / 1e9
     kernels = {k: {"ms_per_step": round(ms / args.steps, 3), "launches_per_step": round(n / args.steps, 1),
                    "avg_launch_ms": round(ms / n, 4) if n else None}
                for k, (ms, n) in ktimes.items() if n}
-    dominant = None
-    if "trace" in ktimes and ktimes["trace"][1]:
-        t_ms, t_n = ktimes["trace"]
-        per_launch = (B_PER_CROSSING * C + 8.0 * S) * per_gpu * args.steps / t_n
-        dominant = {"name": "k_trace", "alg_bytes_per_packet": round(B_PER_CROSSING * C + 8.0 * S, 1),
-                    "alg_bytes_per_launch": round(per_launch), "avg_launch_ms": round(t_ms / t_n, 4),
-                    "achieved_gbs": round(per_launch / (t_ms / t_n * 1e-3) / 1e9, 2),
-                    "bound": "VALU issue (valu_issue below), not HBM"}
-    traffic = None
-    if os.path.exists(args.pmc_json):
+    # the whole transport of one step is a pipeline of launches (k_trace / k_event / k_emit
+    # per iteration): B_alg over the summed launch durations
+    k_ms = sum(ms for ms, _ in ktimes.values()) / args.steps
+    pipeline_gbs = b_alg * per_gpu / (k_ms * 1e-3) / 1e9
+    # the roofline is quoted for the DOMINANT kernel, k_trace: its share of B_alg (the kappa
+    # gather of every crossing, 8 B, and the albedo read at every interaction, 8 B) times the
+    # packets one launch carries, over its average launch duration (HIP events, timed region)
+    t_ms, t_n = ktimes.get("trace", (0.0, 0))
+    trace_bpp = B_PER_CROSSING * C + 8.0 * S
+    per_launch = trace_bpp * per_gpu * args.steps / t_n if t_n else 0.0
+    avg_ms = t_ms / t_n if t_n else float("nan")
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9 if t_n else 0.0
+    # HBM traffic of k_trace from the PMC passes (tools/gpu_round.sh): only when they profiled
+    # THIS build of the library (its md5 is recorded in the summary), else null
+    traffic, traffic_src, limiter = None, None, None
+    lib_md5 = _md5(os.path.join(ROOT, "artes_amd", "lib", "libartes_hip.so"))
+    for path, key in ((args.pmc_json, "pmc"), (args.sq_json, "sq")):
         try:
-            pmc = json.load(open(args.pmc_json))
-            traffic = float(pmc["hbm_bytes_per_packet"]) * per_gpu
+            prof = json.load(open(path))
         except Exception:
-            traffic = None
+            continue
+        if prof.get("lib_md5") != lib_md5:
+            continue
+        kt = {k: v for k, v in prof.get("kernels", {}).items() if k.startswith("k_trace")}
+        if key == "pmc" and kt:
+            bpp = next(iter(kt.values())).get("fabric_bytes_per_packet")
+            if bpp:
+                traffic = round(bpp * per_gpu * args.steps / t_n) if t_n else None
+                traffic_src = os.path.relpath(path, ROOT)
+        if key == "sq" and kt:
+            limiter = {"source": os.path.relpath(path, ROOT), **next(iter(kt.values()))}
+    err_rate = {str(i): {"count": int(e), "per_packet": float(e) / n_step} for i, e in enumerate(err_h) if e}
 
     # Stokes-I parity against the frozen reference run (tests/golden): one more step of the
     # same workload, untimed, with the packet-level moments the honest per-pixel errors need
@@ -227,14 +260,6 @@ def main() -> int:
                   "sample": "one untimed-region step on rank 0, same workload otherwise"}
         g32.close()
 
-    # what bounds k_trace (committed SQ counter passes, tools/pmc_sq_summary.py)
-    compute = None
-    if os.path.exists(args.sq_json):
-        try:
-            compute = {"source": os.path.relpath(args.sq_json, ROOT), **json.load(open(args.sq_json))["kernels"]}
-        except Exception:
-            compute = None
-
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(atm, params)
@@ -254,29 +279,29 @@ def main() -> int:
         "data": "synthetic (uniform Rayleigh atmosphere, generated in-process; no checkpoint/dataset)",
         "config": {"workload": "BASELINE configs[2]: Rayleigh 16-element Mueller, 32x16x32 (r,theta,phi), 1 wavelength, "
                                "star source, imaging_mono 25x25, tau=1",
-                   "packets_per_gpu_per_step": per_gpu, "parallelism": f"packet-sharded x{world}, RCCL detector all-reduce"},
+                   "packets_per_gpu_per_step": per_gpu,
+                   "parallelism": f"packet-sharded x{world}" + (f", one {backend} sum all_reduce per step"
+                                                                 if backend else ", single process")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     # measured L2<->fabric bytes of the committed PMC passes over this step's transport time
-                     "traffic_gbs": round(traffic / (k_ms * 1e-3) / 1e9, 2) if traffic else None,
-                     "kernel": "transport pipeline per step (k_trace + k_event + k_emit + aux launches)",
-                     "kernel_ms": round(k_ms, 3), "step_ms_hip_events": round(float(np.mean(step_ms)), 3),
-                     "kernels": kernels,
-                     "bytes_per_packet_alg": round(b_alg, 1),
-                     # the dominant kernel alone: its share of B_alg (the kappa gather of every
-                     # crossing and the albedo read at every interaction) over its launches
-                     "dominant_kernel": dominant,
+                     "kernel": "k_trace (dominant: cell-boundary tracing)",
+                     "alg_bytes_per_packet": round(trace_bpp, 1), "alg_bytes_per_launch": round(per_launch),
+                     "avg_launch_ms": round(avg_ms, 4), "launches": t_n,
+                     "traffic_source": traffic_src,
+                     # what actually limits k_trace (SQ counter passes of this build), if profiled
+                     "limiter": limiter,
+                     "pipeline": {"kernels": kernels, "ms_per_step": round(k_ms, 3),
+                                  "alg_bytes_per_packet": round(b_alg, 1), "achieved_gbs": round(pipeline_gbs, 2),
+                                  "step_ms_hip_events": round(float(np.mean(step_ms)), 3)},
                      "events_per_packet": {"crossings": round(C, 3), "scatters": round(S, 4), "peels": round(P, 4)}},
         "cpu_baseline": cpu,
         "parity": parity,
         "grid_32cubed": grid32,
-        "valu_issue": compute,
-        "errors": {str(i): int(e) for i, e in enumerate(err_h) if e},
+        # reference error codes (error.log numbers) logged in the timed steps, with their rate
+        "errors": err_rate,
     }
     print(json.dumps(out), flush=True)
     if world > 1:
-        import torch.distributed as tdist
-
         tdist.barrier()
     return 0
 

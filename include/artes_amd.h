@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define ARTES_ABI_VERSION 4
+#define ARTES_ABI_VERSION 5
 #define ARTES_NUM_TOTALS 10
 #define ARTES_NUM_ERR 64
 
@@ -203,8 +203,11 @@ int32_t artes_set_profiling(artes_grid* grid, int32_t on);
 int32_t artes_kernel_times(artes_grid* grid, double* ms, uint64_t* launches);
 
 /* Debug: per-packet records for packets [first, first+n) (n <= 2^24):
- * rec[n][4] = { sum of peeled I weight, scatters, crossings, end state }.
+ * rec[n][ARTES_TRACE_FIELDS] = { sum of peeled I weight, scatters, crossings,
+ * end state (1 exit, 2 absorbed, 3 dropped), sum of peeled -Q, U, V (the detector's
+ * sign convention, ARTES.f90:4953-4960), 0 }.
  * Used by the parity tests to compare trajectories with the CPU oracle. */
+#define ARTES_TRACE_FIELDS 8
 int32_t artes_run_trace(artes_grid* grid, const artes_run_params* params,
                         uint64_t first_packet, uint64_t n_packets, uint64_t seed,
                         double* records);

@@ -101,7 +101,8 @@ typedef struct ctx {
     uint64_t* cnt;         /* thread-private [ARTES_NUM_COUNTERS] */
     double* detector;      /* thread-private [4][4][ny][nx] */
     double* totals;        /* thread-private [8] */
-    double peel_sum;       /* per-packet trace record */
+    double peel_sum;       /* per-packet trace record: peeled Stokes I */
+    double peel_pol[3];    /* per-packet trace record: peeled -Q, U, V (detector sign, ARTES.f90:4956) */
     int cur_pix;           /* pixel of the packet's running contribution (-1: none) */
     double cur_sum[4];     /* running contribution of this packet to cur_pix */
     double pkt_tot[4];     /* this packet's total detected weight */
@@ -766,6 +767,7 @@ static void peel_photon(ctx* X, double xp, double yp, double zp, const double st
         for (int k = 0; k < 4; k++) X->cur_sum[k] += v[k];
         X->cnt[ARTES_CNT_DETECTED]++;
         X->peel_sum += wI;
+        for (int k = 0; k < 3; k++) X->peel_pol[k] += v[k + 1];
     } else {
         error_log(X, 53);
     }
@@ -1062,6 +1064,7 @@ static int transport_packet(ctx* X, uint64_t seed, uint64_t id, double* nscat_ou
     int face[2], cell[3];
     X->cnt[ARTES_CNT_PACKETS]++;
     X->peel_sum = 0.0;
+    X->peel_pol[0] = X->peel_pol[1] = X->peel_pol[2] = 0.0;
     *nscat_out = 0.0;
     const int planet = (p->photon_source == 2);
     if (planet) {                                  /* ARTES.f90:599-622 */
@@ -1139,7 +1142,8 @@ static int transport_packet(ctx* X, uint64_t seed, uint64_t id, double* nscat_ou
 }
 
 /* Run packets [first, first+n). detector [4][4][ny][nx], totals[ARTES_NUM_TOTALS], counters, err are ACCUMULATED into.
- * records (optional) [n][4] = {peeled I sum, scatters, crossings, end state}. */
+ * records (optional) [n][ARTES_TRACE_FIELDS] = {peeled I sum, scatters, crossings, end state,
+ * peeled -Q, U, V sums, 0} (artes_run_trace). */
 int oracle_run_flow(const oracle_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
                     int nthreads, double* detector, double* totals, uint64_t* counters, uint64_t* err, double* records,
                     double* flow_global, double* flow_latitudinal);
@@ -1218,11 +1222,15 @@ int oracle_run_flow(const oracle_grid* g, const artes_run_params* p, uint64_t fi
             int endst = transport_packet(&X, seed, first + (uint64_t)i, &nscat);
             end_packet_stats(&X);
             if (records) {
-                double* rec = records + (size_t)i * 4;
+                double* rec = records + (size_t)i * ARTES_TRACE_FIELDS;
                 rec[0] = X.peel_sum;
                 rec[1] = nscat;
                 rec[2] = (double)(X.cnt[ARTES_CNT_CROSSINGS] - c0);
                 rec[3] = (double)endst;
+                rec[4] = X.peel_pol[0];
+                rec[5] = X.peel_pol[1];
+                rec[6] = X.peel_pol[2];
+                rec[7] = 0.0;
             }
         }
     }

@@ -11,7 +11,8 @@ import subprocess
 
 import numpy as np
 
-from artes_amd.abi import ARTES_NUM_COUNTERS, ARTES_NUM_ERR, ARTES_NUM_TOTALS, GridArrays, GridDesc, RunParams
+from artes_amd.abi import (ARTES_NUM_COUNTERS, ARTES_NUM_ERR, ARTES_NUM_TOTALS, ARTES_TRACE_FIELDS, GridArrays, GridDesc,
+                           RunParams)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liboracle.so")
@@ -76,7 +77,7 @@ class OracleGrid:
         tot = np.zeros(ARTES_NUM_TOTALS)
         cnt = np.zeros(ARTES_NUM_COUNTERS, dtype=np.uint64)
         err = np.zeros(ARTES_NUM_ERR, dtype=np.uint64)
-        rec = np.zeros((n, 4)) if records else None
+        rec = np.zeros((n, ARTES_TRACE_FIELDS)) if records else None
         rc = lib().oracle_run(self.h, C.byref(params), first, n, seed, threads,
                               det.ctypes.data_as(C.POINTER(C.c_double)), tot.ctypes.data_as(C.POINTER(C.c_double)),
                               cnt.ctypes.data_as(C.POINTER(C.c_uint64)), err.ctypes.data_as(C.POINTER(C.c_uint64)),

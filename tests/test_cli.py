@@ -91,6 +91,58 @@ def test_spectrum_and_phase_modes(tmp_path):
     assert len(rows) == 73 and float(rows[0].split()[0]) == 0.0 and float(rows[-1].split()[0]) == 180.0
 
 
+def test_imaging_broad_accumulates_and_scales_by_last_wavelength(tmp_path):
+    """imaging_broad (ARTES.f90:168-204): the thread sums accumulate over the wavelengths
+    (array_start only at wl_count == 1) and each call rescales them by the CURRENT
+    wavelength's package energy (959-975), so stokes.fits = sum_lambda(raw sums) x E(last),
+    sum w^2 x E(last)^2; normalization.dat has the last wavelength only."""
+    from artes_amd import driver
+    from oracle.oracle import OracleGrid
+
+    wls = (0.5, 0.7, 0.9)
+    _make_input(tmp_path, mode="imaging_broad", name="ray3d", nr=6, ntheta=4, nphi=4, wavelength=wls)
+    n, seed = 6000, 21
+    assert runner.run(["atm", str(n), "-o", "bb", "--seed", str(seed)], root=str(tmp_path),
+                      transport_factory=OracleTransport) == 0
+    out = tmp_path / "output" / "bb" / "output"
+    stokes = fitsio.read(out / "stokes.fits")[0].data
+    err = fitsio.read(out / "error.fits")[0].data
+    assert not (out / "photometry.dat").exists() and not (out / "spectrum.dat").exists()
+    norm = np.loadtxt(out / "normalization.dat", ndmin=2)
+    assert norm.shape[0] == 1 and norm[0, 0] == pytest.approx(0.9)
+    # the same packets by hand: call k transports the global ids [k n, (k+1) n)
+    atm = atmosphere.read_atmosphere_fits(str(tmp_path / "input" / "atm" / "atmosphere.fits"))
+    cfg = driver.default_config()
+    rt = float(atm["radial"][-1])
+    det = driver.detector_geometry(cfg, rt)
+    g = OracleGrid(atm)
+    acc = 0.0
+    for k in range(len(wls)):
+        p = driver.run_params(cfg, det, k, cell_depth=g.cell_depth(k), packet_moments=False)
+        acc = acc + g.run(p, k * n, n, seed, threads=4)[0][:3]
+    E = [driver.package_energy(cfg, w * 1e-6, rt, n, det.det_phi) for w in wls]
+    assert len(set(E)) == 3                                  # the energies differ per wavelength
+    np.testing.assert_allclose(stokes, acc[0] * E[-1] * 1e-6 / det.pixel_scale ** 2, rtol=1e-12, atol=0)
+    want = driver.scale_detector(acc, E[-1])
+    assert np.all(want[1] == acc[1] * E[-1] ** 2)
+    np.testing.assert_allclose(err, driver.error_image(want), rtol=1e-12, atol=0)
+    assert stokes[0].sum() > 0
+
+
+@pytest.mark.gpu
+def test_imaging_broad_gpu_matches_oracle_cli(tmp_path, require_gpu):
+    """The same imaging_broad run on the HIP engine and on the oracle (same seeds): the
+    images are sums over the same packets."""
+    _make_input(tmp_path, mode="imaging_broad", name="ray3d", nr=8, ntheta=6, nphi=8, wavelength=(0.5, 0.7, 0.9))
+    assert runner.run(["atm", "3e4", "-o", "g", "--seed", "8"], root=str(tmp_path)) == 0
+    assert runner.run(["atm", "3e4", "-o", "o", "--seed", "8"], root=str(tmp_path), transport_factory=OracleTransport) == 0
+    g = fitsio.read(tmp_path / "output/g/output/stokes.fits")[0].data
+    o = fitsio.read(tmp_path / "output/o/output/stokes.fits")[0].data
+    scale = np.abs(o[0]).max()
+    np.testing.assert_allclose(g, o, rtol=1e-3, atol=1e-3 * scale)
+    assert o[0].sum() > 0 and (tmp_path / "output/g/error.log").read_text() == ""
+
+
 def _make_thermal_input(root, mode="imaging_mono"):
     d = root / "input" / "hot"
     d.mkdir(parents=True)

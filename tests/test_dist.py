@@ -33,6 +33,8 @@ def transport(first, n, seed):
     return RunResult(d, t, c, e, fg, ft)
 
 res = dist.run_sharded(transport, 30001, 99, r)
+seed = dist.broadcast_int((2**62 + 12345) if r.rank == 0 else 777, r)   # the CLI's clock seed
+open({out!r}.replace("det2.npy", "seed%d.txt" % r.rank), "w").write(str(seed))
 if r.rank == 0:
     open({out!r}.replace("det2.npy", "backend.txt"), "w").write(tdist.get_backend())
     np.save({out!r}, res.det)
@@ -62,6 +64,7 @@ def test_two_rank_gloo_equals_single_process(tmp_path):
     for pr in procs:
         assert pr.wait(timeout=300) == 0
     assert open(str(tmp_path / "backend.txt")).read() == "gloo"
+    assert [int(open(str(tmp_path / f"seed{k}.txt")).read()) for k in range(2)] == [2**62 + 12345] * 2
     det2 = np.load(out)
     cnt2 = np.load(out.replace(".npy", "_cnt.npy"))
 

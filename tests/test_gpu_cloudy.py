@@ -18,7 +18,7 @@ by far less than that)."""
 import numpy as np
 import pytest
 
-from artes_amd import atmosphere, driver, runner, synthetic
+from artes_amd import atmosphere, driver, runner, stats, synthetic
 
 pytestmark = pytest.mark.gpu
 
@@ -32,8 +32,7 @@ def cloudy(tmp_path_factory):
 
 
 def _same(gpu, ref):
-    return (np.isclose(gpu[:, 0], ref[:, 0], rtol=1e-9, atol=1e-300) & (gpu[:, 1] == ref[:, 1])
-            & (gpu[:, 2] == ref[:, 2]) & (gpu[:, 3] == ref[:, 3]))
+    return stats.records_agree(gpu, ref)
 
 
 @pytest.mark.parametrize("wl", [0, 1, 2])
@@ -55,6 +54,9 @@ def test_cloudy_trajectories_match_oracle(require_gpu, oracle_mod, cloudy, wl):
     short = ref[:, 1] <= 20
     assert same[short].mean() >= 0.999 and same.mean() >= 0.99, (wl, same.mean(), same[short].mean())
     assert gpu[:, 1].mean() > 2.0              # several scatterings per packet in the cloud
+    # the Mie matrix has P34 != 0, so multiple scattering turns U into V: the per-packet
+    # comparison of V (records_agree) is not a comparison of zeros (~1/3 of the packets)
+    assert (np.abs(ref[:, 6]) > 1e-6 * np.abs(ref[:, 0])).mean() > 0.1
 
 
 def test_cloudy_detector_lds_knob(require_gpu, cloudy):

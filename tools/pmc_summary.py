@@ -14,12 +14,18 @@ requests (HBM and Infinity-Cache hits alike); on gfx950 FETCH_SIZE counts half t
 of wide coalesced reads, so bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  For the
 8-byte gathers of this engine the factor 2 is an upper-bound correction.
 usage: python tools/pmc_summary.py <prof_dir> <packets_in_profiled_run> <out.json>
+The md5 of the profiled libartes_hip.so is recorded: bench.py quotes the traffic only for
+the build that was profiled.
 """
 import csv
+import hashlib
 import json
 import os
 import sys
 from collections import defaultdict
+
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "artes_amd", "lib", "libartes_hip.so")
 
 
 def rows(path):
@@ -57,6 +63,7 @@ def main():
         "hbm_bytes_total": hbm, "hbm_bytes_per_packet": hbm / packets,
         "transport_ms_total": sum(v["total_ms"] for v in kernels.values()),
         "kernels": kernels,
+        "lib_md5": hashlib.md5(open(LIB, "rb").read()).hexdigest(),
         "note": "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 summed over all artes:: kernels of the profiled "
                 "bench run (L2<->fabric requests: HBM and Infinity Cache)",
     }
