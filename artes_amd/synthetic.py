@@ -151,3 +151,47 @@ def make_thermal(kind: str = "ray", nr: int = 16, ntheta: int = 8, nphi: int = 8
     t = temperature(rc) if callable(temperature) else np.full(nr, float(temperature))
     atm["temperature"] = np.broadcast_to(np.asarray(t, dtype=np.float64)[None, None, :], shape).copy()
     return atm
+
+
+SELF_LUMINOUS_IN = """[grid]
+radius: 1.
+radial:
+theta: {theta}
+phi: {phi}
+
+[composition]
+gas: on
+molweight: 2.02
+log_g: 3.4
+ring:
+"""
+
+
+def make_self_luminous(directory: str, fixture: str, theta: str = "30, 60, 90, 120, 150",
+                       phi: str = "90, 180, 270", wavelengths=None) -> dict:
+    """BASELINE configs[4]'s input: a self-luminous gas atmosphere with P-T dependent
+    molecular opacities, built through the reference's setup path from a committed
+    opacity fixture (``tests/golden/molecular``, made by tools/make_molecular_fixture.py
+    from dat/molecules with ``artes_amd.gas.molecule_opacities``, i.e. opacityMolecules.py).
+
+    Writes ``directory`` = ``input/<atm>/`` as the reference's scripts would:
+    ``pressureTemperature.dat`` (pressureTemperatureSelfLuminous.py), one
+    ``opacity/gas_opacity_NN.fits`` per P-T layer (opacity from the fixture, H2 Rayleigh
+    matrices regenerated, opacityMolecules.py:291-300) and an ``atmosphere.in`` with the gas
+    branch on (a ``theta`` x ``phi`` grid over the radial layers), then runs
+    ``artes_amd.atmosphere.build`` (atmosphere.py), which writes ``atmosphere.fits``.
+    ``wavelengths``: optional index subset of the fixture's wavelengths."""
+    from . import atmosphere, gas
+
+    z = np.load(fixture)
+    opd = os.path.join(directory, "opacity")
+    os.makedirs(opd, exist_ok=True)
+    gas.write_pt_file(directory, z["pressure"], z["temperature"])
+    sel = slice(None) if wavelengths is None else np.asarray(wavelengths)
+    for layer, opacity in zip(z["layers"], z["opacity"]):
+        o = np.ascontiguousarray(opacity[:, sel])
+        op.write_opacity_fits(os.path.join(opd, "gas_opacity_%02d.fits" % int(layer)), o,
+                              gas.rayleigh_matrix_table(0.0, o.shape[1]))
+    with open(os.path.join(directory, "atmosphere.in"), "w") as f:
+        f.write(SELF_LUMINOUS_IN.format(theta=theta, phi=phi))
+    return atmosphere.build(directory)
