@@ -57,146 +57,160 @@ __device__ __forceinline__ double fast_sqrt(double x) {
 }
 
 // ---------------------------------------------------- face tables (LDS) ---
-// fv[0..nr] = rfront^2, fv[nr+1 .. nr+1+ntheta] = tan^2(theta_f): one array so the
-// radial and theta families read their two face values with the same instruction;
-// tfl[k] = theta-face flags; phsc[2k], phsc[2k+1] = sin, cos(phi_k)
-constexpr int TF_CONE = 1, TF_GT90 = 2, TF_LT90 = 4;
+// The spheres and the theta cones are one quadric form along the ray,
+//     ax2 x^2 + by2 y^2 + w cz2 z^2 - off = 0,
+// with (w, off) = (1, rfront^2) for a radial face and (-tan^2(theta_f), 0) for a theta
+// face (ARTES.f90:2885-3010, 3014-3290).  A face record is {w, off, s, pl}: s is the
+// cone's nappe sign (+1: theta_f > 90 deg, a root with z > 0 is on the other nappe;
+// -1: theta_f < 90 deg, z < 0 is; 0: radial faces and the 90-degree plane) and pl = 1
+// marks the 90-degree plane (tplane = 2).  The records of the radial faces 0..nr are
+// followed by those of the theta faces 0..ntheta, so every family reads its two faces
+// with the same instructions and no per-lane select of coefficients or flags (the phi
+// family reads radial records, whose s and pl are 0); phsc[k] = (sin, cos)(phi_k).
+struct alignas(32) FaceRec {
+    double w, off, s, pl;
+};
 
 struct TraceTabs {
-    const double* fv;
-    const double* phsc;
-    const int* tfl;
+    const FaceRec* fr;
+    const double2* phsc;
 };
 
 __host__ __device__ inline size_t trace_table_bytes(int nr, int ntheta, int nphi) {
-    return sizeof(double) * ((size_t)(nr + 1) + (size_t)(ntheta + 1) + 2 * (size_t)nphi) + sizeof(int) * (size_t)(ntheta + 1);
+    return sizeof(FaceRec) * ((size_t)(nr + 1) + (size_t)(ntheta + 1)) + sizeof(double2) * (size_t)nphi;
 }
 
 __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double* lds) {
     TraceTabs T;
-    double* fv = lds;
-    for (int i = threadIdx.x; i <= G.nr; i += BLOCK) fv[i] = G.rf2[i];
-    for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) fv[G.nr + 1 + i] = G.tan2[i];
-    double* phsc = fv + (G.nr + 1) + (G.ntheta + 1);
-    for (int i = threadIdx.x; i < G.nphi; i += BLOCK) { phsc[2 * i] = G.phis[i]; phsc[2 * i + 1] = G.phic[i]; }
-    int* tfl = (int*)(phsc + 2 * G.nphi);
+    FaceRec* fr = (FaceRec*)lds;
+    for (int i = threadIdx.x; i <= G.nr; i += BLOCK) fr[i] = FaceRec{1.0, G.rf2[i], 0.0, 0.0};
     for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) {
         const double th = G.thetaf[i];
-        tfl[i] = (G.tplane[i] == 1 ? TF_CONE : 0) | (th > HALF_PI ? TF_GT90 : 0) | (th < HALF_PI ? TF_LT90 : 0);
+        const bool cone = G.tplane[i] == 1;
+        fr[G.nr + 1 + i] = FaceRec{-G.tan2[i], 0.0, cone ? (th > HALF_PI ? 1.0 : (th < HALF_PI ? -1.0 : 0.0)) : 0.0,
+                                   cone ? 0.0 : 1.0};
     }
+    double2* phsc = (double2*)(fr + (G.nr + 1) + (G.ntheta + 1));
+    for (int i = threadIdx.x; i < G.nphi; i += BLOCK) phsc[i] = make_double2(G.phis[i], G.phic[i]);
     __syncthreads();
-    T.fv = fv; T.phsc = phsc; T.tfl = tfl;
+    T.fr = fr; T.phsc = phsc;
     return T;
 }
 
+// min of two doubles that are never NaN (roots, or the +inf "no candidate"): one v_min_f64,
+// without the canonicalising v_max the IEEE-mode fmin needs on unknown operands
+__device__ __forceinline__ double min_nonan(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+constexpr double INF = __builtin_inf();
+
 // ------------------------------------------------------- family evaluation ---
-// Candidate distances to the inner and outer face of ONE coordinate family of cell
+// Nearest crossing ahead among the inner and outer face of ONE coordinate family of cell
 // (cr, ct, cp) from (x, y, z) along n, for a packet sitting on face (ft, fi):
 //   fam 0: spheres r_cr, r_cr+1   (ARTES.f90:2885-3010)
 //   fam 1: theta cones / the 90-degree plane, faces ct, ct+1 (3014-3290)
-//   fam 2: phi half-planes cp, cp+1 (3292-3350)
-// 0 = no candidate, as in the reference.  zp = distance to the plane z = 0.
+//   fam 2: phi half-planes cp, pout (3292-3350)
+// Returns the distance (+inf: no candidate) and whether it is the outer face.  zp = the
+// distance to the plane z = 0; Axy = ax2 n0^2 + by2 n1^2, Az = cz2 n2^2 (per trace).
+//
+// Per face k (0 inner, 1 outer) the reference's rules reduce to: two roots a_k, b_k
+// (phi planes and the 90-degree plane: one), each a candidate when it exists, lies on the
+// right nappe (cones), exceeds the face's tolerance and is < 1e100; none when both exist
+// and are equal, or when a per-face veto (same-face and grid-edge rules) applies; the
+// nearer candidate wins (quadratic_equation + cell_face root choice, ARTES.f90:2885-3350,
+// 4154-4173).  Absent candidates are +inf, so the choice is one min.  The 1e100 cap of
+// the chosen root is applied per root: the nearer root of a pair is below 1e100 iff
+// the reference's choice is.  A root exists when its divisor exceeds 1e-100 in
+// magnitude (the reference's |den| > 0 for the phi planes differs only where num/den is
+// >= 1e100 anyway; the sp0 quirk keeps |den| > 0).  The conditions are written as
+// monotone AND/OR of comparisons (no selects of booleans), which stay lane masks.
 template <bool G3D, bool OBL>
-__device__ __forceinline__ void family_candidates(const DevGrid& G, const TraceTabs& T, int fam, double x, double y,
-                                                  double z, double n0, double n1, double n2, int ft, int fi, int cr,
-                                                  int ct, int cp, double zp, double& d_in, double& d_out) {
+__device__ __forceinline__ double family_eval(const DevGrid& G, const TraceTabs& T, int fam, double x, double y, double z,
+                                              double n0, double n1, double n2, double Axy, double Az, int ft, int fi,
+                                              int cr, int ct, int cp, int pout, double zp, bool& outer) {
     const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
     const bool isR = !G3D || fam == 0;
     const bool isT = G3D && fam == 1;
     const bool isP = G3D && fam == 2;
-    // sphere:  ax2 x^2 + by2 y^2 + cz2 z^2 - r^2        (w = 1,       off = r^2)
-    // cone:    ax2 x^2 + by2 y^2 - cz2 z^2 tan^2(theta) (w = -tan^2, off = 0)
-    const double Axy = ax2 * n0 * n0 + by2 * n1 * n1, Az = cz2 * n2 * n2;
     const double Bxy = ax2 * x * n0 + by2 * y * n1, Bz = cz2 * z * n2;
     const double Cxy = ax2 * x * x + by2 * y * y, Cz = cz2 * z * z;
-    const int kin = isR ? cr : ct;
-    const int vb = isR ? 0 : G.nr + 1;
-    const double vin = T.fv[vb + kin], vout = T.fv[vb + kin + 1];
-    const double win = isR ? 1.0 : -vin, wout = isR ? 1.0 : -vout;
-    const double qa0 = Axy + win * Az, qb0 = 2.0 * (Bxy + win * Bz), qc0 = Cxy + win * Cz - (isR ? vin : 0.0);
-    const double qa1 = Axy + wout * Az, qb1 = 2.0 * (Bxy + wout * Bz), qc1 = Cxy + wout * Cz - (isR ? vout : 0.0);
+    const int kin = isT ? ct : cr;
+    const int e = (isT ? G.nr + 1 : 0) + kin;
+    const FaceRec fin = T.fr[e], fout = T.fr[e + 1];
+    // radial-only grids: w = 1 (spheres only), no nappe sign, no plane
+    const double w0 = G3D ? fin.w : 1.0, w1 = G3D ? fout.w : 1.0;
+    const double s0 = G3D ? fin.s : 0.0, s1 = G3D ? fout.s : 0.0;
+    const double qa0 = fma(w0, Az, Axy), qb0 = 2.0 * fma(w0, Bz, Bxy), qc0 = fma(w0, Cz, Cxy) - fin.off;
+    const double qa1 = fma(w1, Az, Axy), qb1 = 2.0 * fma(w1, Bz, Bxy), qc1 = fma(w1, Cz, Cxy) - fout.off;
     // quadratic_equation (ARTES.f90:4154-4173), both faces
     const double disc0 = qb0 * qb0 - 4.0 * qa0 * qc0, disc1 = qb1 * qb1 - 4.0 * qa1 * qc1;
     const double q0 = -0.5 * (qb0 + copysign(fast_sqrt(disc0), qb0));
     const double q1 = -0.5 * (qb1 + copysign(fast_sqrt(disc1), qb1));
     // phi half-planes: num / den per face (ARTES.f90:3300-3346)
     double num0 = 0.0, den0 = 1.0, num1 = 0.0, den1 = 1.0;
-    int pout = 0;
     if constexpr (G3D) {
         const double ga = OBL ? G.a : 1.0, gb = OBL ? G.b : 1.0;
-        pout = (cp + 1 == G.nphi) ? 0 : cp + 1;
-        const double s0 = T.phsc[2 * cp], c0 = T.phsc[2 * cp + 1];
-        const double s1 = T.phsc[2 * pout], c1 = T.phsc[2 * pout + 1];
-        den0 = gb * n1 * c0 - ga * n0 * s0; num0 = ga * x * s0 - gb * y * c0;
-        den1 = gb * n1 * c1 - ga * n0 * s1; num1 = ga * x * s1 - gb * y * c1;
+        const double2 sc0 = T.phsc[cp], sc1 = T.phsc[pout];
+        den0 = gb * n1 * sc0.y - ga * n0 * sc0.x; num0 = ga * x * sc0.x - gb * y * sc0.y;
+        den1 = gb * n1 * sc1.y - ga * n0 * sc1.x; num1 = ga * x * sc1.x - gb * y * sc1.y;
     }
-    // four divisions shared by the families: quadratic roots q/a and c/q, or the two
-    // plane intersections num/den
-    const double ra0 = fast_div(isP ? num0 : q0, isP ? den0 : qa0);
-    const double rb0 = fast_div(qc0, q0);
-    const double ra1 = fast_div(isP ? num1 : q1, isP ? den1 : qa1);
-    const double rb1 = fast_div(qc1, q1);
-    // Per face k (0 inner, 1 outer) the reference's rules reduce to: two roots a_k, b_k
-    // (phi planes and the 90-degree plane: one), each a candidate when it exists, lies
-    // on the right nappe (cones) and exceeds the face's tolerance; the nearer candidate
-    // wins, none if both are equal or the winner is >= 1e100 (quadratic_equation +
-    // cell_face root choice, ARTES.f90:2885-3350, 4154-4173); and a per-face veto
-    // (same-face and grid-edge rules).  Absent candidates are +inf and the choice is
-    // one min, so the wave executes one selection per face instead of one per family
-    // and rule.  The phi and 90-degree-plane rules keep their own cap (none) and
-    // tolerance (0) exactly.
+    // four divisions shared by the families: the roots q/a and c/q, or the plane
+    // intersections num/den
+    const double da0 = isP ? den0 : qa0, da1 = isP ? den1 : qa1;
+    const double a0r = fast_div(isP ? num0 : q0, da0);
+    const double b0 = fast_div(qc0, q0);
+    const double a1r = fast_div(isP ? num1 : q1, da1);
+    const double b1 = fast_div(qc1, q1);
     const int kout = kin + 1;
     const int kin_f = isP ? cp : kin, kout_f = isP ? pout : kout;
-    const int ftype = isR ? 1 : (isT ? 2 : 3);
-    const bool same0 = (ft == ftype && fi == kin_f), same1 = (ft == ftype && fi == kout_f);
-    const int fl0 = T.tfl[isT ? kin : 0], fl1 = T.tfl[isT ? kout : 0];
-    const bool plane0 = isT && !(fl0 & TF_CONE), plane1 = isT && !(fl1 & TF_CONE);
-    // roots and their existence
-    const bool q_ok0 = disc0 >= 0.0, q_ok1 = disc1 >= 0.0;
-    bool va0 = isP ? fabs(den0) > 0.0 : (q_ok0 && fabs(qa0) > 1.e-100);
-    bool vb0 = !isP && q_ok0 && fabs(q0) > 1.e-100;
-    bool va1 = isP ? fabs(den1) > 0.0 : (q_ok1 && fabs(qa1) > 1.e-100);
-    bool vb1 = !isP && q_ok1 && fabs(q1) > 1.e-100;
-    // cone nappe filter (ARTES.f90:3040-3064): a root on the other nappe is no crossing
-    // (the reference's `s > 1e-15` guard is implied by the tolerance test below)
-    if (isT) {
-        const bool gt0 = fl0 & TF_GT90, lt0 = fl0 & TF_LT90, gt1 = fl1 & TF_GT90, lt1 = fl1 & TF_LT90;
-        const double za0 = fma(ra0, n2, z), zb0 = fma(rb0, n2, z), za1 = fma(ra1, n2, z), zb1 = fma(rb1, n2, z);
-        va0 = va0 && !((za0 > 0.0 && gt0) || (za0 < 0.0 && lt0));
-        vb0 = vb0 && !((zb0 > 0.0 && gt0) || (zb0 < 0.0 && lt0));
-        va1 = va1 && !((za1 > 0.0 && gt1) || (za1 < 0.0 && lt1));
-        vb1 = vb1 && !((zb1 > 0.0 && gt1) || (zb1 < 0.0 && lt1));
+    const bool onfam = ft == fam + 1;
+    const bool same0 = onfam & (fi == kin_f), same1 = onfam & (fi == kout_f);
+    const bool plane0 = G3D && fin.pl != 0.0, plane1 = G3D && fout.pl != 0.0;   // (theta lanes only)
+    // existence: the divisor, and for the quadratic the discriminant
+    const bool d_ok0 = isP | (disc0 >= 0.0), d_ok1 = isP | (disc1 >= 0.0);
+    bool va0 = d_ok0 & (fabs(da0) > 1.e-100);
+    bool vb0 = !isP & (disc0 >= 0.0) & (fabs(q0) > 1.e-100);
+    bool va1 = d_ok1 & (fabs(da1) > 1.e-100);
+    bool vb1 = !isP & (disc1 >= 0.0) & (fabs(q1) > 1.e-100);
+    // cone nappe filter (ARTES.f90:3040-3064): a root on the other nappe is no crossing;
+    // s = 0 (radial records, the plane) never rejects
+    if constexpr (G3D) {
+        va0 = va0 & !(s0 * fma(a0r, n2, z) > 0.0);
+        vb0 = vb0 & !(s0 * fma(b0, n2, z) > 0.0);
+        va1 = va1 & !(s1 * fma(a1r, n2, z) > 0.0);
+        vb1 = vb1 & !(s1 * fma(b1, n2, z) > 0.0);
     }
-    // the 90-degree plane: one root at zp, moving towards it (ARTES.f90:3066-3070, 3116-3118)
-    const double a0 = plane0 ? zp : ra0, a1 = plane1 ? zp : ra1;
-    if (plane0) { va0 = n2 > 1.e-15; vb0 = false; }
-    if (plane1) { va1 = n2 < -1.e-15; vb1 = false; }
     // tolerances: re-crossing the face the packet sits on needs 1e-3 m (spheres: outer
-    // face only, cones: both; ARTES.f90:2944, 3157), 1e-15 otherwise, 0 for the plane
-    const double tol0 = plane0 ? 0.0 : ((same0 && isT) ? 1.e-3 : 1.e-15);
-    const double tol1 = plane1 ? 0.0 : ((same1 && !isP) ? 1.e-3 : 1.e-15);
-    va0 = va0 && a0 > tol0; vb0 = vb0 && rb0 > tol0;
-    va1 = va1 && a1 > tol1; vb1 = vb1 && rb1 > tol1;
+    // face only, cones: both; ARTES.f90:2944, 3157), 1e-15 otherwise; the 90-degree plane
+    // has one root at zp, valid when moving towards it (ARTES.f90:3066-3070, 3116-3118)
+    const bool big0 = same0 & isT, big1 = same1 & !isP;
+    const double a0 = plane0 ? zp : a0r, a1 = plane1 ? zp : a1r;
+    va0 = (va0 & !plane0 & (a0 > 1.e-15) & (!big0 | (a0 > 1.e-3))) | (plane0 & (n2 > 1.e-15) & (a0 > 0.0));
+    va1 = (va1 & !plane1 & (a1 > 1.e-15) & (!big1 | (a1 > 1.e-3))) | (plane1 & (n2 < -1.e-15) & (a1 > 0.0));
+    vb0 = vb0 & !plane0 & (b0 > 1.e-15) & (!big0 | (b0 > 1.e-3));
+    vb1 = vb1 & !plane1 & (b1 > 1.e-15) & (!big1 | (b1 > 1.e-3));
     // vetoes
     //   spheres: the inner sphere the packet sits on (ARTES.f90:2899-2960)
     //   theta:   the grid's polar faces; a cone the packet sits on unless the root lies
     //            beyond the apex side it faces; the plane it sits on (3014-3290)
     //   phi:     the half-plane the packet sits on; the outer one also when the inner
     //            face's root is >= 1e100 (sic: sp0, ARTES.f90:3318, 3346)
-    const bool sp0_big = !(same0) && fabs(den0) > 0.0 && !(ra0 < 1.e100);
-    const bool kill0 = isR ? same0
-                     : isT ? (ct == 0 || (same0 && (plane0 || !(fl0 & TF_GT90))))
-                           : same0;
-    const bool kill1 = isR ? false
-                     : isT ? (kout == G.ntheta || (same1 && (plane1 || !(fl1 & TF_LT90))))
-                           : (same1 || sp0_big);
-    constexpr double INF = __builtin_inf();
-    const double m0 = fmin(va0 ? a0 : INF, vb0 ? rb0 : INF);
-    const double m1 = fmin(va1 ? a1 : INF, vb1 ? rb1 : INF);
-    const bool z0 = kill0 || (va0 && vb0 && a0 == rb0) || !(m0 < 1.e100);
-    const bool z1 = kill1 || (va1 && vb1 && a1 == rb1) || !(m1 < 1.e100);
-    d_in = z0 ? 0.0 : m0;
-    d_out = z1 ? 0.0 : m1;
+    const bool kill0 = (same0 & !isT) | (isT & ((ct == 0) | (same0 & (plane0 | !(s0 > 0.0)))));
+    const bool sp0_big = isP & !same0 & (fabs(den0) > 0.0) & !(a0r < 1.e100);
+    const bool kill1 = (isT & ((kout == G.ntheta) | (same1 & (plane1 | !(s1 < 0.0))))) | (isP & same1) | sp0_big;
+    // equal roots give no crossing; the 1e100 cap
+    const bool eq0 = va0 & vb0 & (a0 == b0), eq1 = va1 & vb1 & (a1 == b1);
+    va0 = va0 & !kill0 & !eq0 & (a0 < 1.e100);
+    vb0 = vb0 & !kill0 & !eq0 & (b0 < 1.e100);
+    va1 = va1 & !kill1 & !eq1 & (a1 < 1.e100);
+    vb1 = vb1 & !kill1 & !eq1 & (b1 < 1.e100);
+    const double m0 = min_nonan(va0 ? a0 : INF, vb0 ? b0 : INF);
+    const double m1 = min_nonan(va1 ? a1 : INF, vb1 ? b1 : INF);
+    outer = m1 < m0;   // ties: the inner face, as the reference's candidate order
+    return min_nonan(m0, m1);
 }
 
 // Energy-transport diagnostics of a propagation segment (output:flow_global /
@@ -229,6 +243,12 @@ __device__ __noinline__ void flow_segment(double* flow_g, double* flow_t, int ce
 // registers (position, direction, RNG state, Stokes I); the slot is written back once
 // when the chain ends, so no transition waits on memory.
 //
+// Per family the distance from the current position to its nearest face ahead is kept
+// in a register (e0 radial, e1 theta, e2 phi; +inf: none) together with its side (bit f
+// of `sides`: 0 inner, 1 outer face).  A step re-evaluates only the family crossed last
+// (`pending`), picks the nearest of the three, moves there and subtracts the step from
+// the other two.  The linear cell index is updated with the crossing, not recomputed.
+//
 // FLOW instantiations add the energy-transport diagnostics to propagation segments.
 template <bool G3D, bool OBL, int WPE, bool FLOW = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G, DevRun R, Pool S, Lists L) {
@@ -242,7 +262,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
     TraceCursor cur = make_cursor(n, R.static_q64);
     const int fam_all = !G3D ? 1 : (G.nphi > 1 ? 7 : 3);
-    constexpr double NONE = -1.e300;
+    const int nrt = G.nr * G.ntheta;        // linear-index stride of phi
     bool have = false;
 #ifdef ARTES_DEBUG_LANES
     unsigned long long dbg_steps = 0, dbg_lanes = 0, dbg_refills = 0, dbg_tsteps = 0, dbg_tlanes = 0;
@@ -251,11 +271,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     int slot = -1, mode = 0, pcell = 0, pface = 0, ncross = 0;
     double px = 0, py = 0, pz = 0, ttgt = 0, wI = 0;
     Rng rng{0, 0};
-    int tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0, pending = 0;
-    double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, tpar = 0, inz = 0;
-    // per family (radial, theta, phi) the nearest face ahead as a trace parameter, and its
+    int tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0, pending = 0, cell = 0;
+    double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, inz = 0, Axy = 0, Az = 0;
+    // extinction and albedo of the current cell, loaded when the cell changes: the L2 round
+    // trip overlaps the next iteration's face evaluation (one 16-byte load at a 32-bit byte
+    // offset; ncell < 2^28, checked at grid creation)
+    double kext = 0, alb = 0;
+    auto load_cell = [&]() {
+        const double2 kv = *(const double2*)((const char*)G.ka + ((unsigned)cell << 4));
+        kext = kv.x;
+        alb = kv.y;
+    };
+    // per family (radial, theta, phi) the distance to the nearest face ahead, and its
     // side (bit f of `sides`: 0 inner, 1 outer face)
-    double m0 = NONE, m1 = NONE, m2 = NONE;
+    double e0 = INF, e1 = INF, e2 = INF;
     int sides = 0;
     uint32_t c_cross = 0, c_peel = 0;
     // backward propagation after the forced first interaction (see the FIRST-trace end).
@@ -265,16 +294,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     int kb = 0;
     int parked = 0;   // 1: waiting for the batched forced first interaction (3: after a cell error)
 
+    // per-trace constants of the direction, and a fresh family cache
+    auto set_direction = [&](double d0, double d1, double d2) {
+        nx = d0; ny = d1; nz = d2;
+        const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
+        Axy = ax2 * nx * nx + by2 * ny * ny;
+        Az = cz2 * nz * nz;
+        tacc = 0.0;
+        pending = fam_all;
+        e0 = INF; e1 = INF; e2 = INF;
+        if constexpr (G3D) inz = fast_rcp(nz);
+    };
     // a trace starts at the packet position with zero optical depth
     auto start_trace = [&](double d0, double d1, double d2) {
         tx = px; ty = py; tz = pz;
         unpack_cell(pcell, tcr, tct, tcp);
         unpack_face(pface, tft, tfi);
-        nx = d0; ny = d1; nz = d2;
-        tacc = 0.0;
-        tpar = 0.0;
-        pending = fam_all;
-        if constexpr (G3D) inz = fast_rcp(nz);
+        cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
+        load_cell();
+        set_direction(d0, d1, d2);
     };
 
     // The forced first interaction at the end of a first trace (ARTES.f90:658-685): one
@@ -293,32 +331,37 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         // The propagation that follows walks the first trace's chord again, from its start
         // to optical depth tau (ARTES.f90:689-720).  When the interaction lies in the
         // chord's far half it is reached in fewer cells from the far end: walk back from
-        // where the first trace stopped (tx, tft, tfi: set when the lane parked) to optical
-        // depth tau_first - tau.  Same cells in reverse, so the same interaction point up to
-        // rounding; crossing counts are kept as the forward walk's (kb).  Not with the flow
-        // diagnostics (segment order).
+        // where the first trace stopped (tx, tft, tfi, cell: set when the lane parked) to
+        // optical depth tau_first - tau.  Same cells in reverse, so the same interaction
+        // point up to rounding; crossing counts are kept as the forward walk's (kb).  Not
+        // with the flow diagnostics (segment order).
         bool back = false;
         if constexpr (!FLOW) back = R.backward && mid && !err && tau_first - tau < tau;
         kb = back ? 2 * ncross + (ncross - kb) + 1 : 0;
         if (back) {
             ttgt = fmax(tau_first - tau, 0.0);   // tau rounds to <= tau_first + 1 ulp
-            nx = -nx; ny = -ny; nz = -nz;
-            tacc = 0.0;
-            tpar = 0.0;
-            pending = fam_all;
-            if constexpr (G3D) inz = fast_rcp(nz);
+            set_direction(-nx, -ny, -nz);
         } else {
             ttgt = tau;
             start_trace(nx, ny, nz);
         }
     };
 
+    // watchdog: a wave runs ~1e5 iterations per launch at the largest pool; a schedule bug
+    // must not leave waves spinning on the device (the run then fails with error 62)
+    unsigned int iters = 0;
     for (;;) {
+        if (++iters > (1u << 24)) {
+            if ((threadIdx.x & 63) == 0) atomicAdd(&R.err[ARTES_ERR_WATCHDOG], 1ULL);
+            break;
+        }
         {
             const unsigned long long pk = __ballot(parked != 0);
             if (pk) {
                 const int stepping = __popcll(__ballot(have && parked == 0));
-                if (__popcll(pk) >= R.batch || stepping < R.batch_min || cur.exhausted) {
+                // (stepping == 0: every busy lane is parked, and the idle ones may be too few to
+                // refill -- waiting for more would never end)
+                if (__popcll(pk) >= R.batch || stepping < R.batch_min || stepping == 0 || cur.exhausted) {
                     if (parked) {
                         first_interaction(parked & 2);
                         parked = 0;
@@ -360,93 +403,89 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #endif
         int end = 0;   // 0: continue, else the slot's new mode
         if (have && !parked) {
-            // extinction and albedo of the current cell: issued first so the L2 round trip
-            // overlaps the face evaluation (the cell is known before the step)
-            const int cell = tcr + G.nr * (tct + G.ntheta * tcp);
-            // one 16-byte load at a 32-bit byte offset (ncell < 2^28, checked at grid creation)
-            const double2 kv = *(const double2*)((const char*)G.ka + ((unsigned)cell << 4));
-            const double k = kv.x;
-            const double alb = kv.y;
+            const double k = kext;
             // ------------------------------------------- evaluate one face family
             const int fam = G3D ? __builtin_ctz(pending) : 0;
-            double din, dout;
-            family_candidates<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, tft, tfi, tcr, tct, tcp, -tz * inz, din, dout);
-            // the evaluated family's nearest face ahead goes to the cache: the other face of a
-            // family only matters while the packet sits on the first (and then the family
-            // is evaluated again)
-            const bool uo = dout > 0.0 && !(din > 0.0 && din <= dout);
-            const double dm = uo ? dout : din;
-            const double tm = dm > 0.0 ? tpar + dm : NONE;
-            if (fam == 0) m0 = tm;
+            const int pout = G3D ? ((tcp + 1 == G.nphi) ? 0 : tcp + 1) : 0;
+            bool outer;
+            const double dm = family_eval<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp,
+                                                    pout, -tz * inz, outer);
             if constexpr (G3D) {
-                if (fam == 1) m1 = tm;
-                if (fam == 2) m2 = tm;
+                e0 = fam == 0 ? dm : e0;
+                e1 = fam == 1 ? dm : e1;
+                e2 = fam == 2 ? dm : e2;
+                sides = (sides & ~(1 << fam)) | ((outer ? 1 : 0) << fam);
+            } else {
+                e0 = dm;
+                sides = outer ? 1 : 0;
             }
-            sides = (sides & ~(1 << fam)) | ((uo ? 1 : 0) << fam);
             pending &= pending - 1;
             if (pending == 0) {
                 // ------------------------------------------------ trace step
-                // candidates: both faces of the family just evaluated (exact distances) and
-                // the cached nearest face of each other family; `which` = family + 3 * side
-                double e0 = -1.0, e1 = -1.0, e2 = -1.0;
-                if constexpr (G3D) {
-                    e0 = fam == 0 ? -1.0 : m0 - tpar;
-                    e1 = fam == 1 ? -1.0 : m1 - tpar;
-                    e2 = fam == 2 ? -1.0 : m2 - tpar;
-                }
                 // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
-                double best = 1.e100;
-                int which = -1;
-#define ARTES_CONSIDER(dd, w, thr) if ((dd) > (thr) && (dd) < best) { best = (dd); which = (w); }
-#define ARTES_PASS(thr)                                                                    \
-                ARTES_CONSIDER(din, fam, thr)                                              \
-                ARTES_CONSIDER(dout, fam + 3, thr)                                         \
-                if constexpr (G3D) {                                                       \
-                    ARTES_CONSIDER(e0, 0 + 3 * (sides & 1), thr)                           \
-                    ARTES_CONSIDER(e1, 1 + 3 * ((sides >> 1) & 1), thr)                    \
-                    ARTES_CONSIDER(e2, 2 + 3 * ((sides >> 2) & 1), thr)                    \
+                double best;
+                int w = 0;
+                {
+                    const double t0 = e0 > 1.e-9 ? e0 : INF;
+                    best = t0;
+                    if constexpr (G3D) {
+                        const double t1 = e1 > 1.e-9 ? e1 : INF, t2 = e2 > 1.e-9 ? e2 : INF;
+                        if (t1 < best) { best = t1; w = 1; }
+                        if (t2 < best) { best = t2; w = 2; }
+                    }
                 }
-                ARTES_PASS(1.e-9)
-                if (which < 0) {
-                    best = 1.e100;
-                    ARTES_PASS(1.e-12)
+                if (best == INF) {   // rare: nothing beyond 1e-9 m
+                    best = e0 > 1.e-12 ? e0 : INF;
+                    w = 0;
+                    if constexpr (G3D) {
+                        if (e1 > 1.e-12 && e1 < best) { best = e1; w = 1; }
+                        if (e2 > 1.e-12 && e2 < best) { best = e2; w = 2; }
+                    }
                 }
-#undef ARTES_PASS
-#undef ARTES_CONSIDER
-                // next_cell (ARTES.f90:2671-2798)
-                int nft = 0, nfi = -999, ncr = tcr, nct = tct, ncp = tcp;
-                bool err = false;
-                switch (which) {
-                    case 0: nft = 1; nfi = tcr; ncr = tcr - 1; break;
-                    case 3: nft = 1; nfi = tcr + 1; ncr = tcr + 1; break;
-                    case 1: nft = 2; nfi = tct; nct = tct - 1; break;
-                    case 4: nft = 2; nfi = tct + 1; nct = tct + 1; break;
-                    case 2: nft = 3; nfi = tcp; ncp = (tcp == 0) ? G.nphi - 1 : tcp - 1; break;
-                    case 5: nft = 3; { const int po = (tcp + 1 == G.nphi) ? 0 : tcp + 1; nfi = po; ncp = po; } break;
-                    default: err = true; log_err(R, 31); break;
+                // next_cell (ARTES.f90:2671-2798): the crossed family's index moves by one
+                // (phi wraps); the face index is the old one (inner face) or the new one
+                // (outer face) for every family
+                const bool side = (sides >> w) & 1;
+                const int kf = !G3D ? tcr : (w == 0 ? tcr : (w == 1 ? tct : tcp));
+                int kn = kf + (side ? 1 : -1);
+                if constexpr (G3D) {
+                    if (w == 2) kn = kn < 0 ? G.nphi - 1 : (kn == G.nphi ? 0 : kn);
                 }
-                const bool exit = (nft == 1 && nfi == G.nr);
-                if (tft == 1 && tfi == G.cell_depth && nft == 1 && nfi == G.cell_depth) { err = true; log_err(R, 34); }
-                if (ncr < 0) ncr = 0;
+                const int nfi = side ? kn : kf;
+                const bool err31 = !(best < INF);
+                const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
+                const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
+                bool err = err31 | ((tft == 1) & (tfi == G.cell_depth) & surf);
+                if (err31) log_err(R, 31);
+                else if (err) log_err(R, 34);
                 c_cross++;
                 ncross++;
                 const double tau_cell = best * k;
-                const bool surf = (nft == 1 && nfi == G.cell_depth);
                 const bool prop = (mode == S_PROP);
                 const bool hit = prop && tacc + tau_cell > ttgt;
                 const bool stop = err || exit || surf || hit;
                 if constexpr (FLOW) {
                     if (prop && !err && !hit) {   // the segment to the face (ARTES.f90:728-743, 889-904)
-                        const int lat = which == 3 ? 0 : which == 0 ? 1 : which == 4 ? 2 : which == 1 ? 3 : -1;
+                        const int lat = w == 0 ? (side ? 0 : 1) : (w == 1 ? (side ? 2 : 3) : -1);
                         flow_segment(R.flow_g, R.flow_t, cell, tx + best * nx, ty + best * ny, tz + best * nz, nx, ny, nz, best, wI, lat);
                     }
                 }
                 if (!stop) {
                     tacc += tau_cell;
-                    tx += best * nx; ty += best * ny; tz += best * nz;
-                    tpar += best;
-                    tft = nft; tfi = nfi; tcr = ncr; tct = nct; tcp = ncp;
-                    pending = 1 << (which % 3);
+                    tx = fma(best, nx, tx); ty = fma(best, ny, ty); tz = fma(best, nz, tz);
+                    tft = w + 1; tfi = nfi;
+                    if constexpr (G3D) {
+                        tcr = w == 0 ? kn : tcr;
+                        tct = w == 1 ? kn : tct;
+                        tcp = w == 2 ? kn : tcp;
+                        cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
+                        e0 -= best; e1 -= best; e2 -= best;
+                    } else {
+                        cell += kn - kf;
+                        tcr = kn;
+                    }
+                    load_cell();
+                    pending = 1 << w;
                 } else if (prop && !err && hit) {
                     // interaction in this cell (ARTES.f90:705-720), then the scattering-loop
                     // head (788-813): roulette, albedo weight, minimum weight
@@ -501,10 +540,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
                         end = S_END_DROP;
                     } else {
-                        // the forced first interaction waits (parked, at the chord's far end)
+                        // the forced first interaction waits (parked, at the chord's far end:
+                        // the position, face and cell of the crossing, for a backward walk)
                         // until enough lanes of the wave need it (see the top of the loop)
                         tx += best * nx; ty += best * ny; tz += best * nz;
-                        tft = nft; tfi = nfi;
+                        tft = w + 1; tfi = nfi;
                         parked = err ? 3 : 1;
                     }
                 }
@@ -535,9 +575,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         atomicAdd(&R.err[55], dbg_tlanes);
     }
 #endif
-    const unsigned long long w = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);
+    const unsigned long long wv = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);
     if ((threadIdx.x & 63) == 0) {
-        if (w) atomicAdd(&R.cnt[ARTES_CNT_CROSSINGS], w);
+        if (wv) atomicAdd(&R.cnt[ARTES_CNT_CROSSINGS], wv);
         if (wp) atomicAdd(&R.cnt[ARTES_CNT_PEELS], wp);
     }
 }

@@ -505,11 +505,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     const char* env = getenv("ARTES_DEFER");
     R.defer = env ? atoi(env) : 16;
     const char* rf = getenv("ARTES_REFILL");
-    // refill a wave once this many of its lanes are idle: a 3D step (one of three face
-    // families) costs more than a radial-only one, so idle lanes are worth refilling sooner
-    // (ray3d best at 20, radial-only grids at 24, with the static shares below)
+    // refill a wave once this many of its lanes are idle (re-swept after the round-2 step
+    // rewrite: 16 for ray3d and hg, iso flat from 16 to 24)
     const bool grid3d = (T.ntheta > 1 || T.nphi > 1);
-    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? 20 : 24);
+    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : 16;
     const char* ef = getenv("ARTES_EMIT_FIRST");
     R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
     const char* bw = getenv("ARTES_BACKWARD");
@@ -662,10 +661,12 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
         HIP_TRY(hipMemcpy(c, g->d_cnt, sizeof(c), hipMemcpyDeviceToHost));
         for (int i = 0; i < ARTES_NUM_COUNTERS; i++) counters[i] += c[i];
     }
-    if (err) {
+    {
         unsigned long long e[ARTES_NUM_ERR];
         HIP_TRY(hipMemcpy(e, g->d_err, sizeof(e), hipMemcpyDeviceToHost));
-        for (int i = 0; i < ARTES_NUM_ERR; i++) err[i] += e[i];
+        if (err)
+            for (int i = 0; i < ARTES_NUM_ERR; i++) err[i] += e[i];
+        if (e[ARTES_ERR_WATCHDOG]) return fail(-5, "transport kernel watchdog fired: schedule bug, results invalid");
     }
     if (records) HIP_TRY(hipMemcpy(records, g->d_rec, n * ARTES_TRACE_FIELDS * sizeof(double), hipMemcpyDeviceToHost));
     return 0;

@@ -13,6 +13,7 @@ atm = synthetic.make_config(name, share_matrix=True)
 det = driver.detector_geometry(cfg, atm["radial"][-1])
 g = Grid(atm, 0)
 p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0), packet_moments=False)
-g.run(p, 0, 10**5, 1)
+w = g.run(p, 0, 10**5, 1)
 r = g.run(p, 0, n, 2024)
-print(name, n, "kernel ms %.1f -> %.3g pkt/s" % (g.last_kernel_ms(), n / (g.last_kernel_ms() * 1e-3)), flush=True)
+print(name, n, "kernel ms %.1f -> %.3g pkt/s" % (g.last_kernel_ms(), n / (g.last_kernel_ms() * 1e-3)),
+      "crossings (both runs) %d" % (r.counter("crossings") + w.counter("crossings")), flush=True)
