@@ -247,17 +247,53 @@ __device__ __forceinline__ int peel_pixel(const DevRun& R, double px, double py,
     return iy * R.nx + ix;
 }
 
+// Detector accumulation of k_event: planes 0-8 (I Q U V sums, their squares, the peel
+// count) go to `acc` (the block's LDS detector or its HBM copy), plane 9 (the I-only peel
+// count) and the packet moments 12-15 to `det` (the block's HBM copy).  With a one-pixel
+// detector (spectrum / phase, ARTES.f90:453-465) every peel of the grid would add to the
+// same ten addresses, so PIX1 keeps per-lane partial sums in registers instead and
+// reduces them over the wave once, at the end of the kernel (ARTES.f90:4953-4972 sums).
+template <bool PIX1>
+struct DetAcc {
+    double* __restrict__ det;
+    double* __restrict__ acc;
+    size_t plane;
+    double r[10];
+    __device__ __forceinline__ void init(double* d, double* a, size_t pl) {
+        det = d; acc = a; plane = pl;
+#pragma unroll
+        for (int k = 0; k < 10; k++) r[k] = 0.0;
+    }
+    __device__ __forceinline__ void add(int k, int pix, double v) {
+        if constexpr (PIX1) r[k] += v;
+        else if (k == 9) unsafeAtomicAdd(&det[9 * plane + pix], v);   // rare (thermal / surface)
+        else unsafeAtomicAdd(&acc[k * plane + pix], v);
+    }
+    // PIX1: one wave-reduced add per plane (call with the whole wave)
+    __device__ __forceinline__ void flush_wave() {
+        if constexpr (PIX1) {
+#pragma unroll
+            for (int k = 0; k < 10; k++) {
+                const double v = wave_sum_f64(r[k]);
+                if ((threadIdx.x & 63) == 0 && v != 0.0) unsafeAtomicAdd(&det[k * plane], v);
+            }
+        }
+    }
+};
+
 // a peel that carries Stokes I only (peel_thermal 4577-4583, peel_surface 4684-4690):
 // moments 0 and 4, and the I-only count plane 9 (the reference counts it for I alone)
-__device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
-                                           double* __restrict__ acc, size_t plane, double v, int err_code,
+template <bool PIX1>
+__device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int slot, DetAcc<PIX1>& D, double v, int err_code,
                                            uint32_t& c_det) {
     if (!(v > 0.0 && v < 1.e100)) { log_err(R, err_code); return; }
     const int pix = peel_pixel(R, S.s[slot].px, S.s[slot].py, S.s[slot].pz);
     if (pix < 0) { log_err(R, 63); return; }
-    unsafeAtomicAdd(&acc[0 * plane + pix], v);
-    unsafeAtomicAdd(&acc[4 * plane + pix], v * v);
-    unsafeAtomicAdd(&det[9 * plane + pix], 1.0);   // rare (thermal / surface): straight to the block's HBM copy
+    D.add(0, pix, v);
+    D.add(4, pix, v * v);
+    D.add(9, pix, 1.0);
+    double* __restrict__ det = D.det;
+    const size_t plane = D.plane;
     if (R.moments) {
         const int cur = S.s[slot].cur_pix;
         double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
@@ -285,13 +321,13 @@ __device__ __forceinline__ void surface_normal(const DevGrid& G, double x, doubl
 
 // thermal-emission peel done (ARTES.f90:599-622, 4566-4591), then the first optical
 // depth trace of the packet; returns 1 (next trace) or 2 (dropped)
-__device__ __forceinline__ int event_thermal(const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
-                                             double* __restrict__ acc, size_t plane, uint32_t& c_det) {
+template <bool PIX1>
+__device__ __forceinline__ int event_thermal(const DevRun& R, const Pool& S, int slot, DetAcc<PIX1>& D, uint32_t& c_det) {
     const int m = S.s[slot].mode;
     if (m & FLAG_ERR) { log_err(R, 47); S.s[slot].mode = S_END_DROP; return 2; }
     const double tau = S.s[slot].tpeel;
     if ((m & FLAG_EXIT) && tau < 50.0)
-        add_peel_I(R, S, slot, det, acc, plane, exp(-tau) / (4.0 * PI) * S.s[slot].wI, 51, c_det);
+        add_peel_I(R, S, slot, D, exp(-tau) / (4.0 * PI) * S.s[slot].wI, 51, c_det);
     S.s[slot].mode = S_FIRST;
     return 1;
 }
@@ -320,29 +356,29 @@ __device__ __forceinline__ int event_surface_hit(const DevGrid& G, const DevRun&
 }
 
 // surface peel done (ARTES.f90:4633-4700), then the interrupted propagation resumes
-__device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S, int slot, double* __restrict__ det,
-                                                  double* __restrict__ acc, size_t plane, uint32_t& c_det) {
+template <bool PIX1>
+__device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S, int slot, DetAcc<PIX1>& D, uint32_t& c_det) {
     const int m = S.s[slot].mode;
     const double tau = S.s[slot].tpeel;
     if (!(m & FLAG_ERR) && (m & FLAG_EXIT) && tau < 50.0)
-        add_peel_I(R, S, slot, det, acc, plane, exp(-tau) * S.s[slot].cos_surf / PI * S.s[slot].wI, 52, c_det);
+        add_peel_I(R, S, slot, D, exp(-tau) * S.s[slot].cos_surf / PI * S.s[slot].wI, 52, c_det);
     S.s[slot].mode = S_PROP;
     return 1;
 }
 
-// one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended)
-// `acc` takes planes 0-8 (I Q U V sums, their squares, the peel count)
-// at plane stride `plane`:
-// the block's LDS detector or the global copy; `det` (global) takes moments 12-15
+// one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended); the peel
+// contribution goes to `D` (see DetAcc)
+template <bool PIX1>
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, const Line0& L0,
-                                         double* __restrict__ det, double* __restrict__ acc, size_t plane, uint32_t& c_scat,
-                                         uint32_t& c_det) {
+                                         DetAcc<PIX1>& D, uint32_t& c_scat, uint32_t& c_det) {
     {
+        double* __restrict__ det = D.det;
+        const size_t plane = D.plane;
         const int m = L0.mode;
         if ((m & 0xFF) == S_SURF_HIT) return event_surface_hit(G, R, S, slot);
         const int kind = (m >> PEEL_KIND_SHIFT) & 3;
-        if (kind == 1) return event_thermal(R, S, slot, det, acc, plane, c_det);
-        if (kind == 2) return event_surface_peel(R, S, slot, det, acc, plane, c_det);
+        if (kind == 1) return event_thermal(R, S, slot, D, c_det);
+        if (kind == 2) return event_surface_peel(R, S, slot, D, c_det);
         if (m & FLAG_ERR) { S.s[slot].mode = S_END_DROP; return 2; }
         const double px = L0.px, py = L0.py, pz = L0.pz;
         double dx = L0.dx, dy = L0.dy, dz = L0.dz;
@@ -404,10 +440,10 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                         const double v[4] = {w * so[0], -w * so[1], w * so[2], w * so[3]};   // -Q: ARTES.f90:4956
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
-                            unsafeAtomicAdd(&acc[q * plane + pix], v[q]);
-                            unsafeAtomicAdd(&acc[(4 + q) * plane + pix], v[q] * v[q]);
+                            D.add(q, pix, v[q]);
+                            D.add(4 + q, pix, v[q] * v[q]);
                         }
-                        unsafeAtomicAdd(&acc[8 * plane + pix], 1.0);
+                        D.add(8, pix, 1.0);
                         if (R.moments) {   // packet-level moments (diagnostics, line 1)
                             const int cur = S.s[slot].cur_pix;
                             double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
@@ -482,8 +518,11 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
 #ifndef ARTES_EVENT_WPE
 #define ARTES_EVENT_WPE 2
 #endif
-template <bool LDS_T, bool LDS_D>
+//  PIX1:  a one-pixel detector: per-lane register sums, reduced over the wave at the end
+//         (DetAcc); no LDS detector then.
+template <bool LDS_T, bool LDS_D, bool PIX1 = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, Lists L) {
+    static_assert(!(PIX1 && LDS_D), "a one-pixel detector is reduced in registers");
     extern __shared__ double s_ev[];
     DevGrid G = G0;
     const size_t plane = (size_t)R.nx * R.ny;
@@ -507,6 +546,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
         for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) acc[i] = 0.0;
     }
     if constexpr (LDS_T || LDS_D) __syncthreads();
+    DetAcc<PIX1> D;
+    D.init(det, acc, plane);
     const int n = *L.event_n;
     uint32_t c_scat = 0, c_det = 0;
     const int n_pad = (n + 63) & ~63;   // whole waves iterate together (wave-aggregated appends)
@@ -523,7 +564,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
         const int slot_nn = i + 2 * stride < n ? L.event[i + 2 * stride] : -1;
         Line0 nxt;
         if (slot_n >= 0) nxt = *(const Line0*)(S.s + slot_n);
-        const int dest = slot >= 0 ? event_one(G, R, S, slot, cur, det, acc, plane, c_scat, c_det) : 0;
+        const int dest = slot >= 0 ? event_one<PIX1>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
         if (i < n) L.trace_out[R.emit_first ? S.P - 1 - i : i] = (dest == 1) ? slot : -1;
@@ -532,6 +573,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
         slot_n = slot_nn;
         cur = nxt;
     }
+    D.flush_wave();
     if constexpr (LDS_D) {
         __syncthreads();
         for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) {

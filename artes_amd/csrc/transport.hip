@@ -359,8 +359,12 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     // (the I-only count plane 9 of the rare thermal / surface peels goes straight to HBM):
     // with the scattering tables, 76.7 KB at 25x25 pixels, so two blocks share a CU
     const size_t det_bytes = 9 * (size_t)R.nx * R.ny * sizeof(double);
+    // one-pixel detector (spectrum / phase): per-lane register sums reduced over the wave
+    // (k_event PIX1) instead of same-address atomics; ARTES_PIX1=0 turns it off
+    const char* p1 = getenv("ARTES_PIX1");
+    const bool pix1 = (p1 ? atoi(p1) != 0 : true) && R.nx == 1 && R.ny == 1;
     const char* dl = getenv("ARTES_DET_LDS");
-    const bool det_lds = (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
+    const bool det_lds = !pix1 && (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
     int ev_blocks = side_blocks;
     if (det_lds) {
         const size_t b = (ev_lds ? ev_bytes : 0) + det_bytes;
@@ -404,7 +408,9 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         Lists L = lists(in);
         launch_trace_any<G3D>(g, wpe, trace_bpc, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
-            if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
+            if (pix1 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
+            else if (pix1) hipLaunchKernelGGL((k_event<false, false, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+            else if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds) hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
             else if (det_lds) hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L);
             else hipLaunchKernelGGL((k_event<false, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
@@ -427,8 +433,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     }
     g->last_iterations = it;
     if (getenv("ARTES_VERBOSE"))
-        fprintf(stderr, "[artes] event engine: pool %d, %lld iterations, trace blocks %d, event blocks %d (LDS tables %d, detector %d)\n",
-                P, it, g->trace_blocks, ev_blocks, (int)ev_lds, (int)det_lds);
+        fprintf(stderr, "[artes] event engine: pool %d, %lld iterations, trace blocks %d, event blocks %d (LDS tables %d, detector %d, 1-pixel %d)\n",
+                P, it, g->trace_blocks, ev_blocks, (int)ev_lds, (int)det_lds, (int)pix1);
     return 0;
 }
 

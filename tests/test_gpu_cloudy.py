@@ -15,6 +15,8 @@ scatterings identical to 1e-9, >= 99 % overall); the CLI outputs, being sums ove
 same packets, to 1e-3 relative (a rare packet whose last-ulp history differs moves a sum
 by far less than that)."""
 
+import math
+
 import numpy as np
 import pytest
 
@@ -83,6 +85,37 @@ def test_cloudy_detector_lds_knob(require_gpu, cloudy):
     grid.close()
     np.testing.assert_allclose(b.det, a.det, rtol=1e-9, atol=1e-300)
     assert np.array_equal(b.counters, a.counters)
+
+
+@pytest.mark.parametrize("source", ["star", "planet"])
+def test_one_pixel_register_sums_knob(require_gpu, cloudy, source):
+    """A one-pixel detector (spectrum / phase) reduces the peel sums in registers over the
+    wave (k_event PIX1) instead of same-address atomics: same packets, same sums (to the
+    summation order), counts exact; the planet source covers the I-only thermal peels."""
+    import os
+
+    from artes_amd.engine import Grid
+
+    _, _, atm = cloudy
+    if source == "planet":
+        atm = synthetic.make_thermal(nr=10, ntheta=6, nphi=8, tau_abs=1.0, tau_sca=2.0, temperature=1100.0)
+    cfg = driver.default_config()
+    cfg.apply("detector:type", "phase")
+    cfg.apply("photon:source", source)
+    det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
+    assert det.nx == 1 and det.ny == 1
+    grid = Grid(atm, device=0)
+    p = driver.run_params(cfg, det, 0, det_phi=math.radians(40.0), cell_depth=-1 if source == "planet" else grid.cell_depth(0))
+    a = grid.run(p, 0, 300000, 5)
+    os.environ["ARTES_PIX1"] = "0"
+    try:
+        b = grid.run(p, 0, 300000, 5)
+    finally:
+        os.environ.pop("ARTES_PIX1")
+    grid.close()
+    np.testing.assert_allclose(a.det[:2], b.det[:2], rtol=1e-9, atol=1e-300)
+    np.testing.assert_array_equal(a.det[2], b.det[2])
+    assert np.array_equal(a.counters, b.counters) and a.det[0, 0].sum() > 0
 
 
 ARTES_IN = """photon:source=star
