@@ -31,8 +31,19 @@ tabulated range.
 exists for this generator.  The solver is pinned instead by Mie theory's own
 known answers (tests/test_mie.py): the Rayleigh limit, the extinction paradox, the
 optical theorem, the ``Csca = (1/k^2) int S11 dOmega`` identity, single-sphere
-polarisation identities and the Bohren & Huffman worked example.  The distribution of
-hollow spheres (``fmax > 0``, ``opacityMie.py:15,20``) is not restated and raises.
+polarisation identities and the Bohren & Huffman worked example.
+
+The distribution of hollow spheres (DHS; ``fmax > 0`` with ``nf`` volume fractions,
+``opacityMie.py:15,20``) follows its published definition (Min, Hovenier & de Koter
+2005, A&A 432, 909): every particle of the size distribution becomes a sphere with a
+central vacuum inclusion whose volume fraction f is uniform on ``[0, fmax]``, the material
+volume kept equal to the solid sphere's (outer radius ``r / (1 - f)**(1/3)``, core
+``f**(1/3)`` of that), and the cross sections and matrices are averaged over f with the
+midpoint rule on ``nf`` points.  The coated spheres are solved with Bohren & Huffman's
+BHCOAT recurrences (1983, App. B).  ComputePart's own f quadrature is not known (its
+binary is absent), so this path is parity-unpinned too; tests/test_mie.py pins the
+coated-sphere solver by its limits (equal indices, vanishing core, vacuum mantle), the
+optical theorem and energy conservation, and DHS by its ``fmax -> 0`` limit.
 """
 
 from __future__ import annotations
@@ -139,6 +150,103 @@ def bhmie(x, m: complex, mu):
     return qext, qsca, g, s1, s2
 
 
+def bhcoat(x, y, m1: complex, m2: complex, mu):
+    """Coated spheres: core size parameters ``x`` and index ``m1``, outer size parameters
+    ``y`` (arrays of equal length) and mantle index ``m2``, at scattering-angle cosines
+    ``mu``.  Returns ``qext, qsca, s1, s2`` as :func:`bhmie` (without g).
+
+    Bohren & Huffman's BHCOAT (1983, App. B): the mantle's Riccati-Bessel functions and
+    logarithmic derivatives by upward recurrence, the core's influence through the
+    coefficients A_n, B_n, dropped once it is below 1e-8 (the routine's DEL test); the
+    series is truncated at ``y + 4 y^(1/3) + 2``.  As BHCOAT, meant for weakly absorbing
+    mantles and moderate sizes (the DHS of cloud particles).
+    """
+    x = np.atleast_1d(np.asarray(x, dtype=np.float64))
+    y = np.atleast_1d(np.asarray(y, dtype=np.float64))
+    mu = np.atleast_1d(np.asarray(mu, dtype=np.float64))
+    if np.any(x <= 0) or np.any(y < x):
+        raise ValueError("need 0 < x <= y")
+    m1, m2 = complex(m1), complex(m2)
+    x1, x2, y2 = m1 * x, m2 * x, m2 * y
+    nstop = np.floor(y + 4.0 * np.cbrt(y) + 2.0).astype(np.int64)
+    refrel = m2 / m1
+    coated = np.ones(x.size, dtype=bool)          # BHCOAT's IFLAG = 0
+    delta = 1.0e-8
+    # sizes past their own truncation order keep recurring (their terms are masked out) and
+    # may overflow there: those values never reach an active term
+    with np.errstate(all="ignore"):
+        return _bhcoat_series(x, y, m2, mu, x1, x2, y2, nstop, refrel, coated, delta)
+
+
+def _bhcoat_series(x, y, m2, mu, x1, x2, y2, nstop, refrel, coated, delta):
+    d0x1 = np.cos(x1) / np.sin(x1)
+    d0x2 = np.cos(x2) / np.sin(x2)
+    d0y2 = np.cos(y2) / np.sin(y2)
+    psi0y, psi1y = np.cos(y), np.sin(y)
+    chi0y, chi1y = -np.sin(y), np.cos(y)
+    xi1y = psi1y - 1j * chi1y
+    chi0y2, chi1y2 = -np.sin(y2), np.cos(y2)
+    chi0x2, chi1x2 = -np.sin(x2), np.cos(x2)
+    qext = np.zeros(x.size)
+    qsca = np.zeros(x.size)
+    pi0 = np.zeros(mu.size)
+    pi1 = np.ones(mu.size)
+    s1 = np.zeros((x.size, mu.size), dtype=np.complex128)
+    s2 = np.zeros((x.size, mu.size), dtype=np.complex128)
+    for n in range(1, int(nstop.max()) + 1):
+        act = n <= nstop
+        rn = float(n)
+        psiy = (2.0 * rn - 1.0) * psi1y / y - psi0y
+        chiy = (2.0 * rn - 1.0) * chi1y / y - chi0y
+        xiy = psiy - 1j * chiy
+        d1y2 = 1.0 / (rn / y2 - d0y2) - rn / y2
+        d1x1 = 1.0 / (rn / x1 - d0x1) - rn / x1
+        d1x2 = 1.0 / (rn / x2 - d0x2) - rn / x2
+        chix2 = (2.0 * rn - 1.0) * chi1x2 / x2 - chi0x2
+        chiy2 = (2.0 * rn - 1.0) * chi1y2 / y2 - chi0y2
+        chipx2 = chi1x2 - rn * chix2 / x2
+        chipy2 = chi1y2 - rn * chiy2 / y2
+        ancap = (refrel * d1x1 - d1x2) / (refrel * d1x1 * chix2 - chipx2) / (chix2 * d1x2 - chipx2)
+        bncap = (refrel * d1x2 - d1x1) / (refrel * chipx2 - d1x1 * chix2) / (chix2 * d1x2 - chipx2)
+        brack = np.where(coated, ancap * (chiy2 * d1y2 - chipy2), 0.0)
+        crack = np.where(coated, bncap * (chiy2 * d1y2 - chipy2), 0.0)
+        small = ((np.abs(brack * chipy2) <= delta * np.abs(d1y2)) & (np.abs(brack * chiy2) <= delta)
+                 & (np.abs(crack * chipy2) <= delta * np.abs(d1y2)) & (np.abs(crack * chiy2) <= delta))
+        brack = np.where(small, 0.0, brack)
+        crack = np.where(small, 0.0, crack)
+        coated = coated & ~small
+        dnbar = (d1y2 - brack * chipy2) / (1.0 - brack * chiy2)
+        gnbar = (d1y2 - crack * chipy2) / (1.0 - crack * chiy2)
+        an = ((dnbar / m2 + rn / y) * psiy - psi1y) / ((dnbar / m2 + rn / y) * xiy - xi1y)
+        bn = ((m2 * gnbar + rn / y) * psiy - psi1y) / ((m2 * gnbar + rn / y) * xiy - xi1y)
+        an = np.where(act, an, 0.0)
+        bn = np.where(act, bn, 0.0)
+        qsca += (2.0 * rn + 1.0) * (np.abs(an) ** 2 + np.abs(bn) ** 2)
+        qext += (2.0 * rn + 1.0) * (an.real + bn.real)
+        fn = (2.0 * rn + 1.0) / (rn * (rn + 1.0))
+        tau = rn * mu * pi1 - (rn + 1.0) * pi0
+        s1 += fn * (an[:, None] * pi1[None, :] + bn[:, None] * tau[None, :])
+        s2 += fn * (an[:, None] * tau[None, :] + bn[:, None] * pi1[None, :])
+        pi_next = ((2.0 * rn + 1.0) * mu * pi1 - (rn + 1.0) * pi0) / rn
+        pi0, pi1 = pi1, pi_next
+        psi0y, psi1y = psi1y, psiy
+        chi0y, chi1y = chi1y, chiy
+        xi1y = psi1y - 1j * chi1y
+        chi0x2, chi1x2 = chi1x2, chix2
+        chi0y2, chi1y2 = chi1y2, chiy2
+        d0x1, d0x2, d0y2 = d1x1, d1x2, d1y2
+    qsca *= 2.0 / (y * y)
+    qext *= 2.0 / (y * y)
+    return qext, qsca, s1, s2
+
+
+def dhs_fractions(nf: int, fmax: float) -> np.ndarray:
+    """Vacuum volume fractions of the DHS average: midpoints of ``nf`` equal bins of [0, fmax]."""
+    if nf < 1 or not 0.0 <= fmax < 1.0:
+        raise ValueError("need nf >= 1 and 0 <= fmax < 1")
+    return fmax * (np.arange(nf) + 0.5) / nf
+
+
 def amplitude_to_matrix(s1, s2):
     """Six independent elements (F11, F12, F22, F33, F34, F44) of a sphere's
     scattering matrix from its amplitudes (Bohren & Huffman eq. 4.77)."""
@@ -178,19 +286,42 @@ def size_distribution(nr: int, amin: float = 0.1, amax: float = 5.0, apow: float
     return r, nd * r * w                                   # n(r) dr = n(r) r dln r
 
 
+def _particle(r, k: float, m: complex, mu, fracs):
+    """Size-resolved (qext, qsca, F[180 or len(mu)][6] per size) of solid spheres of radius
+    ``r`` [micron] (fracs None) or of their DHS average: cross-section efficiencies refer to
+    the solid sphere's area pi r^2, so the caller's size weights stay those of the solid
+    particles (the DHS keeps the material volume)."""
+    if fracs is None:
+        qext, qsca, _, s1, s2 = bhmie(k * r, m, mu)
+        return qext, qsca, amplitude_to_matrix(s1, s2)
+    qext = np.zeros(r.size)
+    qsca = np.zeros(r.size)
+    f6 = 0.0
+    for f in fracs:
+        rout = r / (1.0 - f) ** (1.0 / 3.0)
+        if f == 0.0:
+            qe, qs, _, s1, s2 = bhmie(k * rout, m, mu)
+        else:
+            qe, qs, s1, s2 = bhcoat(k * rout * f ** (1.0 / 3.0), k * rout, 1.0 + 0.0j, m, mu)
+        area = (rout / r) ** 2                     # pi rout^2 / pi r^2
+        qext += qe * area / len(fracs)
+        qsca += qs * area / len(fracs)
+        f6 = f6 + amplitude_to_matrix(s1, s2) / len(fracs)
+    return qext, qsca, f6
+
+
 def mie_opacity(refractive_index, wavelengths, density: float = 1.0, nr: int = 1000,
                 amin: float = 0.1, amax: float = 5.0, apow: float = 0.0, fmax: float = 0.0,
-                r_eff: float = 1.4, v_eff: float = 0.05, normalizer: str = "simps"):
+                r_eff: float = 1.4, v_eff: float = 0.05, normalizer: str = "simps", nf: int = 20):
     """``opacityMie.py`` end to end: ``(opacity (4, nwav), scatter (180, 16, nwav))``.
 
     ``refractive_index`` is a path in the reference's ``.dat`` format or a
     ``(wavelength, n, k)`` tuple.  Opacities are per gram of particles
     [cm2 g-1]: size-averaged cross sections over the size-averaged particle mass
-    ``4/3 pi r^3 density``.
+    ``4/3 pi r^3 density``.  ``fmax > 0``: the distribution of hollow spheres with ``nf``
+    volume fractions (module docstring).
     """
-    if fmax > 0.0:
-        raise NotImplementedError("distribution of hollow spheres (fmax > 0) is not restated; "
-                                  "use fmax = 0 (homogeneous spheres)")
+    fracs = dhs_fractions(nf, fmax) if fmax > 0.0 else None
     table = read_refractive_index(refractive_index) if isinstance(refractive_index, str) \
         else tuple(np.asarray(a, dtype=np.float64) for a in refractive_index)
     wavelengths = np.atleast_1d(np.asarray(wavelengths, dtype=np.float64))
@@ -203,7 +334,7 @@ def mie_opacity(refractive_index, wavelengths, density: float = 1.0, nr: int = 1
     six = np.zeros((180, 6, nwav))
     for j, (w, m) in enumerate(zip(wavelengths, refractive_index_at(table, wavelengths))):
         k = 2.0 * math.pi / w
-        qext, qsca, _, s1, s2 = bhmie(k * r, m, mu)
+        qext, qsca, f6 = _particle(r, k, m, mu, fracs)
         area = math.pi * (r * 1e-4) ** 2                                        # cm2
         c_ext = np.sum(wn * qext * area)
         c_sca = np.sum(wn * qsca * area)
@@ -211,7 +342,7 @@ def mie_opacity(refractive_index, wavelengths, density: float = 1.0, nr: int = 1
         opacity[1, j] = c_ext / mass
         opacity[3, j] = c_sca / mass
         opacity[2, j] = opacity[1, j] - opacity[3, j]
-        f = np.einsum("s,sea->ae", wn, amplitude_to_matrix(s1, s2))
+        f = np.einsum("s,sea->ae", wn, f6)
         # per steradian, normalised to the size-averaged scattering cross section
         six[:, :, j] = f / (k * k * np.sum(wn * qsca * math.pi * r * r))
     return opacity, normalize_matrix(expand_six_elements(six), normalizer)

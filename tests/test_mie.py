@@ -95,9 +95,66 @@ def test_distribution_opacity_and_matrix():
     assert opn[1, 0] == pytest.approx(qext * 3 / (4 * r0 * 1e-4), rel=1e-2)   # 1 % spread in r
 
 
-def test_hollow_spheres_not_restated():
-    with pytest.raises(NotImplementedError):
-        mie.mie_opacity((np.array([1.0]), np.array([1.5]), np.array([0.0])), [1.0], fmax=0.8)
+MU = np.cos((np.arange(180) + 0.5) * math.pi / 180.0)
+
+
+@pytest.mark.parametrize("m", [1.5 + 0.01j, 1.33 + 1e-4j, 1.7 + 0.1j])
+def test_coated_sphere_limits(m):
+    """BHCOAT (Bohren & Huffman 1983, App. B) against its exact limits: equal core and
+    mantle indices = a homogeneous sphere of the outer size; a vacuum mantle = a homogeneous
+    sphere of the core size (efficiencies scale with the area); a vanishing vacuum core = a
+    homogeneous sphere of the outer size."""
+    y = np.array([0.3, 2.0, 8.0, 25.0])
+    qe, qs, s1, s2 = mie.bhcoat(0.6 * y, y, m, m, MU)
+    qe0, qs0, _, t1, t2 = mie.bhmie(y, m, MU)
+    np.testing.assert_allclose(qe, qe0, rtol=1e-7)
+    np.testing.assert_allclose(qs, qs0, rtol=1e-7)
+    np.testing.assert_allclose(s1, t1, rtol=0, atol=1e-7 * np.abs(t1).max())
+    np.testing.assert_allclose(s2, t2, rtol=0, atol=1e-7 * np.abs(t2).max())
+    x = 0.7 * y
+    qe, qs, s1, _ = mie.bhcoat(x, y, m, 1.0, MU)
+    qe0, qs0, _, t1, _ = mie.bhmie(x, m, MU)
+    np.testing.assert_allclose(qe * y ** 2, qe0 * x ** 2, rtol=1e-9)
+    np.testing.assert_allclose(s1, t1, rtol=0, atol=1e-9 * np.abs(t1).max())
+    qe, qs, _, _ = mie.bhcoat(1e-4 * y, y, 1.0, m, MU)
+    qe0, qs0, _, _, _ = mie.bhmie(y, m, MU)
+    np.testing.assert_allclose(qe, qe0, rtol=1e-7)
+    np.testing.assert_allclose(qs, qs0, rtol=1e-7)
+
+
+@pytest.mark.parametrize("y", [0.5, 3.0, 15.0])
+def test_coated_sphere_energy_and_optical_theorem(y):
+    qe, qs, s1, _ = mie.bhcoat([0.5 * y], [y], 1.0, 1.5, [1.0])      # non-absorbing mantle
+    assert qe[0] == pytest.approx(qs[0], rel=1e-12)
+    assert qe[0] == pytest.approx(4.0 / y ** 2 * s1[0, 0].real, rel=1e-12)   # optical theorem
+    qe, qs, s1, _ = mie.bhcoat([0.5 * y], [y], 1.0, 1.5 + 0.05j, [1.0])
+    assert qe[0] > qs[0] > 0.0                                          # absorption
+    assert qe[0] == pytest.approx(4.0 / y ** 2 * s1[0, 0].real, rel=1e-10)
+
+
+def test_hollow_sphere_distribution():
+    """DHS (fmax > 0, opacityMie.py:15,20): the fmax -> 0 limit is the homogeneous
+    distribution; voids change the matrix smoothly; material mass (and so the opacity per
+    gram's normalisation) is that of the solid particles."""
+    ri = (np.array([0.5, 2.0]), np.array([1.5, 1.5]), np.array([1e-3, 1e-3]))
+    kw = dict(density=1.0, nr=40, r_eff=0.5, v_eff=0.1)
+    op0, sc0 = mie.mie_opacity(ri, [0.8], **kw)
+    # the void shifts the particle's outer radius by ~f/3 (material volume kept): the
+    # departure from the homogeneous distribution is first order in fmax and vanishes with it
+    d = []
+    for fmax in (1e-5, 1e-6):
+        op1, sc1 = mie.mie_opacity(ri, [0.8], fmax=fmax, nf=4, **kw)
+        np.testing.assert_allclose(op1, op0, rtol=20 * fmax)
+        d.append(np.abs(sc1 - sc0).max() / np.abs(sc0).max())
+    assert d[0] < 1e-4 and 7.0 < d[0] / d[1] < 13.0, d
+    op8, sc8 = mie.mie_opacity(ri, [0.8], fmax=0.8, nf=10, **kw)
+    assert op8[1, 0] > 0 and op8[3, 0] > 0 and op8[1, 0] != pytest.approx(op0[1, 0], rel=1e-3)
+    # normalised matrix: 2 pi int P11 sin = 1 (atmosphere.py:60-65 conventions)
+    ang = (np.arange(180) + 0.5) * math.pi / 180
+    assert 2 * math.pi * np.sum(sc8[:, 0, 0] * np.sin(ang)) * math.pi / 180 == pytest.approx(1.0, rel=2e-3)
+    np.testing.assert_allclose(mie.dhs_fractions(4, 0.8), [0.1, 0.3, 0.5, 0.7])
+    with pytest.raises(ValueError):
+        mie.dhs_fractions(0, 0.5)
 
 
 @need_ri
