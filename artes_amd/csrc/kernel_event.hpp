@@ -92,7 +92,37 @@ struct Lists {
     int* emit;            int* emit_n;
     unsigned int* grab;                 // [8] shard cursors of trace_in
     unsigned long long* next_pkt;       // packets handed out so far
+    int* dbg_owner;                     // ARTES_DEBUG: [P] last (iteration, stage) tag per slot
+    int* dbg_iter;                      // ARTES_DEBUG: iteration counter (k_rotate)
 };
+
+// Work-list invariants of one engine iteration (checked by ARTES_DEBUG builds; a
+// violation counts error ARTES_ERR_LISTS and fails the run):
+//  (L1) every live packet's slot is named exactly once, by one list: the input trace
+//       list (k_trace), then the event list or the emit list (k_trace pushes each slot it
+//       ends to exactly one), then the output trace list (k_event at its event index,
+//       k_emit at event_n + its emit index, or mirrored from position P-1 downwards with
+//       emit_first); a slot no list names is free;
+//  (L2) list entries are slot ids in [0, P) or -1 (a hole: a dropped or retired packet);
+//       a trace-list position read is < trace_in_n and maps into [0, P) (the mirrored
+//       half: P-1-(j-split), j < trace_in_n); event_n + emit_n <= P, so the two writers
+//       of the output trace list never overlap;
+//  (L3) a slot's mode matches its list: a trace kind in the trace list, S_PEEL_DONE /
+//       S_SURF_HIT in the event list, an end state (or S_FRESH at the start) in the emit list.
+// A variant that parks unfinished traces of k_trace's tail must give them list positions
+// of their own (outside [0, event_n + emit_n)) and persist the trace state it drops; both
+// appending them with an atomic counter into positions the other writers also use, and
+// resuming them with the in-register trace state lost, break (L1)/(L2) -- duplicate slots
+// (the trajectory mismatch) and mirrored positions outside [0, P) (a memory fault).
+__device__ __forceinline__ void dbg_claim(const DevRun& R, const Lists& L, int slot, int P, int stage, bool mode_ok) {
+#ifdef ARTES_DEBUG
+    if (slot < -1 || slot >= P || (slot >= 0 && !mode_ok)) { atomicAdd(&R.err[ARTES_ERR_LISTS], 1ULL); return; }
+    if (slot >= 0) {
+        const int tag = 3 * *L.dbg_iter + stage;
+        if (atomicExch(&L.dbg_owner[slot], tag) == tag) atomicAdd(&R.err[ARTES_ERR_LISTS], 1ULL);
+    }
+#endif
+}
 
 // slot modes
 enum SlotMode : int {
@@ -564,6 +594,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
         const int slot_nn = i + 2 * stride < n ? L.event[i + 2 * stride] : -1;
         Line0 nxt;
         if (slot_n >= 0) nxt = *(const Line0*)(S.s + slot_n);
+#ifdef ARTES_DEBUG
+        if (i < n) dbg_claim(R, L, slot, S.P, 1, slot >= 0 && to_event_list(cur.mode));
+#endif
         const int dest = slot >= 0 ? event_one<PIX1>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
@@ -684,6 +717,9 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
     for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
         const int slot = i < n ? L.emit[i] : -1;
         const int m = slot >= 0 ? S.s[slot].mode : S_RETIRED;
+#ifdef ARTES_DEBUG
+        if (i < n) dbg_claim(R, L, slot, S.P, 2, m == S_END_EXIT || m == S_END_ABS || m == S_END_DROP || m == S_FRESH);
+#endif
         if (m == S_END_EXIT || m == S_END_ABS || m == S_END_DROP) {
             if (m == S_END_EXIT) c_exit++;
             else if (m == S_END_ABS) c_abs++;
@@ -828,9 +864,13 @@ __global__ void k_init(Pool S, int* emit, int* emit_n, int use) {
 // emit_n) becomes the input, the consumed input buffer is reset to become the next
 // output, packet ids advance by the emit-list length; event/emit lists and cursors are zeroed
 __global__ void k_rotate(int* in_n, int* out_n, int* out_split, int* event_n, int* emit_n, unsigned int* grab,
-                         unsigned long long* next_pkt, int emit_first) {
+                         unsigned long long* next_pkt, int emit_first, int P, int* dbg_iter, unsigned long long* err) {
     if (threadIdx.x == 0) {
         const int ev = *event_n, em = *emit_n;
+#ifdef ARTES_DEBUG
+        if (ev < 0 || em < 0 || ev + em > P) atomicAdd(&err[ARTES_ERR_LISTS], 1ULL);   // (L2)
+        *dbg_iter += 1;
+#endif
         *out_n = ev + em;
         *out_split = emit_first ? em : ev + em;
         *next_pkt += (unsigned long long)em;

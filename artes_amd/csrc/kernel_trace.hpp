@@ -378,6 +378,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 dbg_refills++;
 #endif
                 if (!have && my >= 0) slot = L.trace_in[my < split ? my : S.P - 1 - (my - split)];
+#ifdef ARTES_DEBUG
+                if (!have && my >= 0) {
+                    const int pos = my < split ? my : S.P - 1 - (my - split);
+                    const int m = (slot >= 0 && slot < S.P) ? S.s[slot].mode : S_FIRST;
+                    dbg_claim(R, L, (my < n && pos >= 0 && pos < S.P) ? slot : -2, S.P, 0, m == S_FIRST || m == S_PROP || is_peel_trace(m));
+                }
+#endif
                 if (!have && my >= 0 && slot >= 0) {   // -1: a hole left by a dropped or retired packet
                     const Slot* rec = S.s + slot;
                     mode = rec->mode;

@@ -96,7 +96,8 @@ struct artes_grid {
     int* d_lists[2] = {nullptr, nullptr};
     int* d_event = nullptr;
     int* d_emit = nullptr;
-    int* d_counts = nullptr;              // [0],[1] trace lists, [2] event, [3] emit
+    int* d_counts = nullptr;              // [0],[1] trace lists, [2] event, [3] emit, [4],[5] splits, [8] debug iteration
+    int* d_owner = nullptr;               // ARTES_DEBUG: [P] slot ownership tags
     unsigned int* d_grab = nullptr;       // [8]
     unsigned long long* d_next = nullptr;
     int* h_count = nullptr;               // pinned
@@ -190,7 +191,8 @@ void artes_grid_destroy(artes_grid* g) {
                     g->d_flow};
     for (void* p : ptrs)
         if (p) hipFree(p);
-    void* eptrs[] = {g->pool_mem, g->d_lists[0], g->d_lists[1], g->d_event, g->d_emit, g->d_counts, g->d_grab, g->d_next};
+    void* eptrs[] = {g->pool_mem, g->d_lists[0], g->d_lists[1], g->d_event, g->d_emit, g->d_counts, g->d_grab, g->d_next,
+                     g->d_owner};
     for (void* p : eptrs)
         if (p) hipFree(p);
     if (g->h_count) hipHostFree(g->h_count);
@@ -301,6 +303,9 @@ static int32_t ensure_pool(artes_grid* g) {
     HIP_TRY(hipMalloc((void**)&g->d_grab, 16 * sizeof(unsigned int)));
     HIP_TRY(hipMalloc((void**)&g->d_next, sizeof(unsigned long long)));
     HIP_TRY(hipHostMalloc((void**)&g->h_count, 64, hipHostMallocDefault));
+#ifdef ARTES_DEBUG
+    HIP_TRY(hipMalloc((void**)&g->d_owner, (size_t)P * sizeof(int)));
+#endif
     HIP_TRY(hipEventCreateWithFlags(&g->ev_poll, hipEventDisableTiming));
     return 0;
 }
@@ -342,6 +347,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     HIP_TRY(hipMemsetAsync(g->d_counts, 0, 16 * sizeof(int), stream));
     HIP_TRY(hipMemsetAsync(g->d_grab, 0, 16 * sizeof(unsigned int), stream));
     HIP_TRY(hipMemsetAsync(g->d_next, 0, sizeof(unsigned long long), stream));
+    if (g->d_owner) HIP_TRY(hipMemsetAsync(g->d_owner, 0xFF, (size_t)P * sizeof(int), stream));   // tags -1: unclaimed
     int* cnt = g->d_counts;
     const int side_blocks = std::max(1, g->num_cus * 8);
     // launch knobs, read once per call (tuning overrides; the defaults are the measured optima)
@@ -380,6 +386,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         L.event = g->d_event; L.event_n = cnt + 2;
         L.emit = g->d_emit; L.emit_n = cnt + 3;
         L.grab = g->d_grab; L.next_pkt = g->d_next;
+        L.dbg_owner = g->d_owner; L.dbg_iter = cnt + 8;
         return L;
     };
     const size_t em_lds = G3D ? emit_table_doubles(G.ntheta, G.nphi) * sizeof(double) : 0;
@@ -397,7 +404,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
             hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + 1, cnt + 0, cnt + 4 + 0, cnt + 2, cnt + 3, g->d_grab, g->d_next,
-                               R.emit_first);
+                               R.emit_first, P, cnt + 8, R.err);
         });
     }
     HIP_TRY(hipGetLastError());
@@ -418,7 +425,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
             hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + in, cnt + (1 - in), cnt + 4 + (1 - in), cnt + 2, cnt + 3,
-                               g->d_grab, g->d_next, R.emit_first);
+                               g->d_grab, g->d_next, R.emit_first, P, cnt + 8, R.err);
         });
         in = 1 - in;
         it++;
@@ -673,6 +680,7 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
         if (err)
             for (int i = 0; i < ARTES_NUM_ERR; i++) err[i] += e[i];
         if (e[ARTES_ERR_WATCHDOG]) return fail(-5, "transport kernel watchdog fired: schedule bug, results invalid");
+        if (e[ARTES_ERR_LISTS]) return fail(-5, "work-list invariant violated (ARTES_DEBUG check): results invalid");
     }
     if (records) HIP_TRY(hipMemcpy(records, g->d_rec, n * ARTES_TRACE_FIELDS * sizeof(double), hipMemcpyDeviceToHost));
     return 0;

@@ -33,10 +33,12 @@
  *   - Functions return 0 on success or a negative errno-style code; they never
  *     exit the process (the reference calls exit(0) on fatal errors).
  *   - Error-code counters: uint64_t err[ARTES_NUM_ERR], index = the reference's
- *     "error NNN" number written to error.log (e.g. ARTES.f90:640, 3401).  Index
- *     ARTES_ERR_WATCHDOG (62, unused by the reference) counts waves of the transport
- *     kernel stopped by the iteration watchdog: the run's results are then invalid and
- *     artes_run / artes_run_flow return -5.
+ *     "error NNN" number written to error.log (e.g. ARTES.f90:640, 3401).  Two
+ *     indices the reference does not use report engine faults, after which the run's
+ *     results are invalid and artes_run / artes_run_flow return -5:
+ *     ARTES_ERR_WATCHDOG (57) counts waves of the transport kernel stopped by its
+ *     iteration watchdog; ARTES_ERR_LISTS (58) counts violations of the work-list
+ *     invariants, checked only by ARTES_DEBUG builds ("Work lists").
  */
 #ifndef ARTES_AMD_H
 #define ARTES_AMD_H
@@ -51,7 +53,8 @@ extern "C" {
 #define ARTES_ABI_VERSION 5
 #define ARTES_NUM_TOTALS 10
 #define ARTES_NUM_ERR 64
-#define ARTES_ERR_WATCHDOG 62
+#define ARTES_ERR_WATCHDOG 57
+#define ARTES_ERR_LISTS 58
 
 /* Counter slots (uint64_t counters[ARTES_NUM_COUNTERS]). */
 #define ARTES_CNT_CROSSINGS 0   /* cell_face calls (ARTES.f90:2800), all traces   */

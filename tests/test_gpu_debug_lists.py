@@ -1,0 +1,66 @@
+"""The work-list invariants of the event engine (kernel_event.hpp, `Lists`: every live slot
+named by exactly one list per stage, positions inside the pool, list modes consistent),
+checked on the GPU by the ARTES_DEBUG build (artes_amd/lib/libartes_hip_debug.so, built by
+__graft_entry__.build()) over schedules that stress the hand-off: tiny pools (hundreds of
+iterations), the mirrored trace-list order, purely dynamic grabs, thermal + surface events
+and a one-pixel detector.  A violation counts error 58 (ARTES_ERR_LISTS) and fails the run;
+the debug build must also transport exactly the release build's packets."""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("ray3d", {}, {}),
+    ("hg", {"ARTES_POOL": "3000", "ARTES_EMIT_FIRST": "1"}, {}),
+    ("ray3d", {"ARTES_POOL": "5000", "ARTES_STATIC": "0", "ARTES_REFILL": "1"}, {}),
+    ("thermal", {"ARTES_POOL": "4000"}, {"photon:source": "planet", "planet:surface_albedo": "0.5"}),
+    ("ray3d", {"ARTES_POOL": "6000"}, {"detector:type": "phase"}),
+]
+
+SCRIPT = r"""
+import json, os, sys
+sys.path.insert(0, {root!r})
+from artes_amd import driver, synthetic
+from artes_amd.engine import Grid
+name, env, kv = json.loads(sys.argv[1])
+os.environ.update(env)
+atm = (synthetic.make_thermal(nr=8, ntheta=4, nphi=6, tau_abs=1.0, tau_sca=1.0) if name == "thermal"
+       else synthetic.make_config(name, **({{}} if name != "ray3d" else dict(nr=8, ntheta=8, nphi=8))))
+cfg = driver.default_config()
+for k, v in kv.items():
+    cfg.apply(k, v)
+det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
+g = Grid(atm, device=0)
+p = driver.run_params(cfg, det, 0, det_phi=0.7 if kv.get("detector:type") == "phase" else None, cell_depth=-1)
+r = g.run(p, 0, 60000, 17)
+print(json.dumps(dict(err=[int(e) for e in r.err], cnt=[int(c) for c in r.counters], det=float(r.det[0].sum()))))
+"""
+
+
+def _run(lib, case):
+    env = dict(os.environ, ARTES_LIB_PATH=lib)
+    out = subprocess.run([sys.executable, "-c", SCRIPT.format(root=ROOT), json.dumps(case)], capture_output=True,
+                         text=True, timeout=120, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_debug_build_list_invariants(require_gpu, case):
+    dbg = os.path.join(ROOT, "artes_amd", "lib", "libartes_hip_debug.so")
+    rel = os.path.join(ROOT, "artes_amd", "lib", "libartes_hip.so")
+    assert os.path.exists(dbg), "build() makes the ARTES_DEBUG library"
+    d = _run(dbg, CASES[case])
+    r = _run(rel, CASES[case])
+    assert d["err"][58] == 0 and d["err"][57] == 0
+    assert d["cnt"] == r["cnt"] and d["cnt"][3] == 60000
+    assert d["det"] == pytest.approx(r["det"], rel=1e-12)
