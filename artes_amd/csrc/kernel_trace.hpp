@@ -27,6 +27,12 @@
 
 #include "device_common.hpp"
 
+#ifdef ARTES_TWOFACE
+static constexpr bool TWOFACE = true;    // A/B builds: evaluate both faces of every family
+#else
+static constexpr bool TWOFACE = false;
+#endif
+
 namespace artes {
 
 // ------------------------------------------------------------ fast math ---
@@ -132,7 +138,7 @@ __device__ __forceinline__ double family_eval(const DevGrid& G, const TraceTabs&
                                               double n0, double n1, double n2, double Axy, double Az, int ft, int fi,
                                               int cr, int ct, int cp, int pout, double zp, bool& outer) {
     const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
-    const bool isR = !G3D || fam == 0;
+    [[maybe_unused]] const bool isR = !G3D || fam == 0;
     const bool isT = G3D && fam == 1;
     const bool isP = G3D && fam == 2;
     const double Bxy = ax2 * x * n0 + by2 * y * n1, Bz = cz2 * z * n2;
@@ -211,6 +217,96 @@ __device__ __forceinline__ double family_eval(const DevGrid& G, const TraceTabs&
     const double m1 = min_nonan(va1 ? a1 : INF, vb1 ? b1 : INF);
     outer = m1 < m0;   // ties: the inner face, as the reference's candidate order
     return min_nonan(m0, m1);
+}
+
+// ------------------------------------------------ one-face family evaluation ---
+// The face of a radial shell or theta band that a straight ray can cross NEXT is known
+// before any root is computed:
+//  * spheres: |p(t)|^2 is convex along the ray.  Moving inwards (p.n < 0) with the ray
+//    reaching the inner sphere (discriminant >= 0), the inner crossing comes first (both
+//    its roots lie ahead, before the perigee, and the outer sphere is only left after
+//    it); otherwise the outer sphere.  The inner sphere the packet sits on is never a
+//    candidate (ARTES.f90:2899-2960), so that case is the outer sphere too.
+//  * theta cones: a line meets any cone level at most twice, so theta(t) has at most one
+//    extremum: the face in the direction theta moves (d cos(theta)/dt ~ n2 C - z B) is the
+//    next one if it is crossed at all; if theta turns back first, that face has no valid
+//    root and the other face is evaluated in the lane's next iteration (`alt`, at most
+//    once per trace).  The same fallback covers the sphere's degenerate cases (a double
+//    root) exactly.
+//  * phi half-planes: both faces, as before (cheap, and the sp0 quirk needs the inner one).
+// So a family costs one quadratic (one square root) instead of two, and the same rules as
+// family_eval's apply to the two roots of the chosen face (for phi: one root per face).
+template <bool G3D, bool OBL>
+__device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs& T, int fam, double x, double y, double z,
+                                               double n0, double n1, double n2, double Axy, double Az, int ft, int fi,
+                                               int cr, int ct, int cp, int pout, double zp, bool alt, bool& outer) {
+    const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
+    const bool isR = !G3D || fam == 0;
+    const bool isT = G3D && fam == 1;
+    const bool isP = G3D && fam == 2;
+    const double Bxy = ax2 * x * n0 + by2 * y * n1, Bz = cz2 * z * n2;
+    const double Cxy = ax2 * x * x + by2 * y * y, Cz = cz2 * z * z;
+    const int kin = isT ? ct : cr;
+    const int e = (isT ? G.nr + 1 : 0) + kin;
+    const bool onfam = ft == fam + 1;
+    const bool same_in = onfam & (fi == (isP ? cp : kin));
+    // which face: the sphere rule needs the inner face's discriminant (w = 1)
+    bool ch;
+    {
+        const double off_in = T.fr[e].off;
+        const double qa_in = Axy + Az, hb = Bxy + Bz, qc_in = Cxy + Cz - off_in;
+        const bool in_ok = (hb < 0.0) & (hb * hb - qa_in * qc_in >= 0.0) & !same_in;
+        ch = isT ? (fma(n2, Cxy + Cz, -z * hb) < 0.0) : !in_ok;
+        ch = ch != alt;
+    }
+    const FaceRec fc = T.fr[e + (ch ? 1 : 0)];
+    const double w = G3D ? fc.w : 1.0, sg = G3D ? fc.s : 0.0;
+    const bool pl = G3D && fc.pl != 0.0;
+    const double qa = fma(w, Az, Axy), qb = 2.0 * fma(w, Bz, Bxy), qc = fma(w, Cz, Cxy) - fc.off;
+    const double disc = qb * qb - 4.0 * qa * qc;
+    const double q = -0.5 * (qb + copysign(fast_sqrt(disc), qb));
+    double num0 = 0.0, den0 = 1.0, num1 = 0.0, den1 = 1.0;
+    if constexpr (G3D) {
+        const double ga = OBL ? G.a : 1.0, gb = OBL ? G.b : 1.0;
+        const double2 sc0 = T.phsc[cp], sc1 = T.phsc[pout];
+        den0 = gb * n1 * sc0.y - ga * n0 * sc0.x; num0 = ga * x * sc0.x - gb * y * sc0.y;
+        den1 = gb * n1 * sc1.y - ga * n0 * sc1.x; num1 = ga * x * sc1.x - gb * y * sc1.y;
+    }
+    // root A: the quadratic's q/a, or phi face 0; root B: c/q, or phi face 1
+    const double dA = isP ? den0 : qa, dB = isP ? den1 : q;
+    const double rA = fast_div(isP ? num0 : q, dA);
+    const double rB = fast_div(isP ? num1 : qc, dB);
+    const bool fA = !isP & ch, fB = isP | ch;                   // faces of the roots (1: outer)
+    const int kA = isP ? cp : kin + (ch ? 1 : 0), kB = isP ? pout : kA;
+    const bool sameA = onfam & (fi == kA), sameB = onfam & (fi == kB);
+    // existence: the divisor, and for the quadratic the discriminant
+    const bool d_ok = isP | (disc >= 0.0);
+    bool vA = d_ok & (fabs(dA) > 1.e-100);
+    bool vB = d_ok & (fabs(dB) > 1.e-100);
+    // cone nappe filter (ARTES.f90:3040-3064); sg = 0 never rejects
+    if constexpr (G3D) {
+        vA = vA & !(sg * fma(rA, n2, z) > 0.0);
+        vB = vB & !(sg * fma(rB, n2, z) > 0.0);
+    }
+    // tolerances (1e-3 m to re-cross the face the packet sits on: spheres outer face only,
+    // cones both; ARTES.f90:2944, 3157); the 90-degree plane: one root at zp, valid when
+    // moving towards it (3066-3070, 3116-3118)
+    const double A = pl ? zp : rA;
+    const bool bigA = sameA & (isT | (isR & fA)), bigB = sameB & (isT | (isR & fB));
+    vA = (vA & !pl & (A > 1.e-15) & (!bigA | (A > 1.e-3))) | (pl & (ch ? (n2 < -1.e-15) : (n2 > 1.e-15)) & (A > 0.0));
+    vB = vB & !pl & (rB > 1.e-15) & (!bigB | (rB > 1.e-3));
+    // vetoes (ARTES.f90:2899-2960, 3014-3290, 3318, 3346)
+    const bool tkill = ch ? ((kin + 1 == G.ntheta) | (sameA & (pl | !(sg < 0.0)))) : ((kin == 0) | (sameA & (pl | !(sg > 0.0))));
+    const bool sp0_big = !sameA & (fabs(den0) > 0.0) & !(rA < 1.e100);
+    const bool killA = (isR & sameA & !fA) | (isT & tkill) | (isP & sameA);
+    const bool killB = (isR & sameB & !fB) | (isT & tkill) | (isP & (sameB | sp0_big));
+    // equal roots of a quadratic give no crossing; the 1e100 cap
+    const bool eq = !isP & vA & vB & (A == rB);
+    vA = vA & !killA & !eq & (A < 1.e100);
+    vB = vB & !killB & !eq & (rB < 1.e100);
+    const double mA = vA ? A : INF, mB = vB ? rB : INF;
+    outer = isP ? (mB < mA) : ch;
+    return min_nonan(mA, mB);
 }
 
 // Energy-transport diagnostics of a propagation segment (output:flow_global /
@@ -292,6 +388,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     // trace that may follow: 2 x crossings at its start + the first trace's steps + 1
     // (from which the forward walk's step count follows at the interaction).  0 otherwise.
     int kb = 0;
+    int tsteps = 0;   // steps of the current trace (runaway guard)
     int parked = 0;   // 1: waiting for the batched forced first interaction (3: after a cell error)
 
     // per-trace constants of the direction, and a fresh family cache
@@ -301,7 +398,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         Axy = ax2 * nx * nx + by2 * ny * ny;
         Az = cz2 * nz * nz;
         tacc = 0.0;
+        tsteps = 0;
         pending = fam_all;
+        sides = 0;
         e0 = INF; e1 = INF; e2 = INF;
         if constexpr (G3D) inz = fast_rcp(nz);
     };
@@ -415,18 +514,31 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             const int fam = G3D ? __builtin_ctz(pending) : 0;
             const int pout = G3D ? ((tcp + 1 == G.nphi) ? 0 : tcp + 1) : 0;
             bool outer;
-            const double dm = family_eval<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp,
-                                                    pout, -tz * inz, outer);
+            // the face the family can cross next; the other one if that has no crossing
+            // (`alt`, bit 4 + fam of `sides`: evaluated in this lane's next iteration).  Both
+            // faces on an oblate grid: there the star's packets start inside the atmosphere's
+            // outer surface (the reference emits them on the unscaled sphere), a position its
+            // cell does not contain, where the nearest crossing is not the one the direction
+            // points to
+            double dm;
+            bool retry = false;
+            if constexpr (OBL || TWOFACE) {
+                dm = family_eval<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, outer);
+            } else {
+                const bool alt = (sides >> (4 + fam)) & 1;
+                dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, outer);
+                retry = (fam != 2) & !alt & !(dm < INF);
+            }
             if constexpr (G3D) {
                 e0 = fam == 0 ? dm : e0;
                 e1 = fam == 1 ? dm : e1;
                 e2 = fam == 2 ? dm : e2;
-                sides = (sides & ~(1 << fam)) | ((outer ? 1 : 0) << fam);
+                sides = (sides & ~(0x11 << fam)) | ((outer ? 1 : 0) << fam) | ((retry ? 1 : 0) << (4 + fam));
             } else {
                 e0 = dm;
-                sides = outer ? 1 : 0;
+                sides = (outer ? 1 : 0) | ((retry ? 1 : 0) << 4);
             }
-            pending &= pending - 1;
+            if (!retry) pending &= pending - 1;
             if (pending == 0) {
                 // ------------------------------------------------ trace step
                 // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
@@ -459,7 +571,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     if (w == 2) kn = kn < 0 ? G.nphi - 1 : (kn == G.nphi ? 0 : kn);
                 }
                 const int nfi = side ? kn : kf;
-                const bool err31 = !(best < INF);
+                bool err31 = !(best < INF);
+                // a trace of 2^22 steps is a schedule or geometry bug, not a history (~100
+                // crossings per packet, a few thousand at most): drop the packet with error
+                // ARTES_ERR_RUNAWAY instead of spinning
+                if (++tsteps > (1 << 22)) {
+                    err31 = true;
+                    log_err(R, ARTES_ERR_RUNAWAY);
+                }
                 const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
                 const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
                 bool err = err31 | ((tft == 1) & (tfi == G.cell_depth) & surf);
@@ -498,6 +617,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     // head (788-813): roulette, albedo weight, minimum weight
                     const double s = fast_div(ttgt - tacc, k);
                     px = tx + s * nx; py = ty + s * ny; pz = tz + s * nz;
+#ifdef ARTES_DEBUG_GEOM
+                    {   // diagnostic build: is the interaction point in the cell's radial shell?
+                        const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
+                        const double S2 = ax2 * px * px + by2 * py * py + cz2 * pz * pz;
+                        if (S2 < G.rf2[tcr] * (1 - 1e-9) || S2 > G.rf2[tcr + 1] * (1 + 1e-9)) {
+                            if (atomicAdd(&R.err[ARTES_ERR_GEOM], 1ULL) < 6)
+                                printf("[geom] hit outside shell: t %.17g %.17g %.17g n %.17g %.17g %.17g cell %d %d %d face %d %d e %.17g %.17g %.17g sides %x s %.17g tsteps %d mode %d S2/rf2 %.17g %.17g\n",
+                                       tx, ty, tz, nx, ny, nz, tcr, tct, tcp, tft, tfi, e0, e1, e2, sides, s, tsteps, mode,
+                                       S2 / G.rf2[tcr], S2 / G.rf2[tcr + 1]);
+                        }
+                    }
+#endif
                     pcell = pack_cell(tcr, tct, tcp);
                     pface = 0;
                     if (kb) {   // a backward trace: count the steps the forward one takes

@@ -339,6 +339,25 @@ static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, 
     }
 }
 
+// diagnostics (ARTES_VERBOSE) when the engine does not terminate: the transport state of
+// the first packets still in the trace list
+static void dump_live(artes_grid* g, const int* d_n, const int* d_list, const int* d_split, int P, hipStream_t stream) {
+    int n = 0, split = 0;
+    if (hipMemcpyAsync(&n, d_n, sizeof(int), hipMemcpyDeviceToHost, stream) != hipSuccess) return;
+    if (hipMemcpyAsync(&split, d_split, sizeof(int), hipMemcpyDeviceToHost, stream) != hipSuccess) return;
+    if (hipStreamSynchronize(stream) != hipSuccess) return;
+    fprintf(stderr, "[artes] live trace list: %d entries (split %d)\n", n, split);
+    for (int j = 0; j < n && j < 8; j++) {
+        const int pos = j < split ? j : P - 1 - (j - split);
+        int slot = -1;
+        Slot r;
+        if (hipMemcpy(&slot, d_list + pos, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || slot < 0 || slot >= P) continue;
+        if (hipMemcpy(&r, g->pool.s + slot, sizeof(Slot), hipMemcpyDeviceToHost) != hipSuccess) continue;
+        fprintf(stderr, "[artes] slot %d pid %llu mode %d p %.17g %.17g %.17g d %.17g %.17g %.17g ttgt %.17g cell %d face %d ncross %d nscat %d wI %.17g\n",
+                slot, r.pid, r.mode, r.px, r.py, r.pz, r.dx, r.dy, r.dz, r.ttgt, r.pcell, r.pface, r.ncross, r.nscat, r.wI);
+    }
+}
+
 template <bool G3D>
 static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R, bool trace, hipStream_t stream) {
     int32_t rc = ensure_pool(g);
@@ -410,7 +429,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     HIP_TRY(hipGetLastError());
     int in = 0;
     long long it = 0;
-    const long long max_it = 2000000LL;
+    const char* mi = getenv("ARTES_MAX_IT");
+    const long long max_it = mi ? atoll(mi) : 2000000LL;
     for (;;) {
         Lists L = lists(in);
         launch_trace_any<G3D>(g, wpe, trace_bpc, G, R, L, stream);
@@ -431,12 +451,20 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         it++;
         if ((it & 7) == 0 || it < 4) {   // poll the live-packet count (trace list of the next iteration)
             HIP_TRY(hipGetLastError());
+            // (and the watchdog counter: a schedule bug fails the run at once instead of
+            // every launch spinning to the watchdog)
+            unsigned long long* h_wd = (unsigned long long*)(g->h_count + 2);
             HIP_TRY(hipMemcpyAsync(g->h_count, cnt + in, sizeof(int), hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipMemcpyAsync(h_wd, R.err + ARTES_ERR_WATCHDOG, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipEventRecord(g->ev_poll, stream));
             HIP_TRY(hipEventSynchronize(g->ev_poll));
+            if (*h_wd) return fail(-5, "transport kernel watchdog fired: schedule bug, results invalid");
             if (*g->h_count == 0) break;
         }
-        if (it > max_it) return fail(-5, "event engine did not terminate");
+        if (it > max_it) {
+            if (getenv("ARTES_VERBOSE")) dump_live(g, cnt + in, g->d_lists[in], cnt + 4 + in, P, stream);
+            return fail(-5, "event engine did not terminate");
+        }
     }
     g->last_iterations = it;
     if (getenv("ARTES_VERBOSE"))
@@ -609,6 +637,7 @@ int32_t artes_run_device_flow(artes_grid* g, const artes_run_params* p, uint64_t
                   cnt_dev ? (unsigned long long*)cnt_dev : g->d_cnt, err_dev ? (unsigned long long*)err_dev : g->d_err,
                   nullptr, s, flow_global_dev, flow_latitudinal_dev);
 }
+
 
 static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first, uint64_t n, uint64_t seed,
                         double* det, double* totals, uint64_t* counters, uint64_t* err, double* records,

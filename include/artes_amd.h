@@ -39,6 +39,11 @@
  *     ARTES_ERR_WATCHDOG (57) counts waves of the transport kernel stopped by its
  *     iteration watchdog; ARTES_ERR_LISTS (58) counts violations of the work-list
  *     invariants, checked only by ARTES_DEBUG builds ("Work lists").
+ *     ARTES_ERR_RUNAWAY (59) counts traces stopped after 2^22 cell crossings (the
+ *     packet is dropped and also counted as error 31); ARTES_ERR_GEOM (60) counts
+ *     interaction points outside their cell's radial shell, checked only by
+ *     ARTES_DEBUG_GEOM builds (a diagnostic: the reference's oblate star emission
+ *     produces such points by design).
  */
 #ifndef ARTES_AMD_H
 #define ARTES_AMD_H
@@ -55,6 +60,8 @@ extern "C" {
 #define ARTES_NUM_ERR 64
 #define ARTES_ERR_WATCHDOG 57
 #define ARTES_ERR_LISTS 58
+#define ARTES_ERR_RUNAWAY 59
+#define ARTES_ERR_GEOM 60
 
 /* Counter slots (uint64_t counters[ARTES_NUM_COUNTERS]). */
 #define ARTES_CNT_CROSSINGS 0   /* cell_face calls (ARTES.f90:2800), all traces   */
