@@ -706,11 +706,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     q_emit.flush(L.emit, L.emit_n);
 #ifdef ARTES_DEBUG_LANES
     if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&R.err[60], dbg_steps);
-        atomicAdd(&R.err[61], dbg_lanes);
-        atomicAdd(&R.err[59], dbg_refills);
-        atomicAdd(&R.err[54], dbg_tsteps);
-        atomicAdd(&R.err[55], dbg_tlanes);
+        // (error slots no reference error uses: 0, 30, 32, 40, 41)
+        atomicAdd(&R.err[0], dbg_steps);
+        atomicAdd(&R.err[30], dbg_lanes);
+        atomicAdd(&R.err[32], dbg_refills);
+        atomicAdd(&R.err[40], dbg_tsteps);
+        atomicAdd(&R.err[41], dbg_tlanes);
     }
 #endif
     const unsigned long long wv = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);

@@ -23,8 +23,8 @@ for name in ("ray3d",):
         g.kernel_times()
         r = g.run(p, 0, n, 2024)
         kt = g.kernel_times()
-        steps, lanes, refills = int(r.err[60]), int(r.err[61]), int(r.err[59])
-        tsteps, tlanes = int(r.err[54]), int(r.err[55])
+        steps, lanes, refills = int(r.err[0]), int(r.err[30]), int(r.err[32])
+        tsteps, tlanes = int(r.err[40]), int(r.err[41])
         C = r.counter("crossings")
         print(f"{name} {env}: {g.last_kernel_ms():.1f} ms ({n / g.last_kernel_ms() / 1e3:.1f} Mpkt/s) trace {kt['trace'][0]:.1f} ms, "
               f"wave-steps {steps:.3e}, lanes/step {lanes / steps:.1f}, crossings/wave-step {C / steps:.1f}, "
