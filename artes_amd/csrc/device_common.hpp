@@ -59,6 +59,7 @@ struct DevRun {
     double det0, det1, det2, sdt, cdt, sdp, cdp;
     double det_phi;                 // atan2(det1, det0) in [0, 2 pi] (peel_photon, ARTES.f90:4868-4870)
     double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
+    double omfstop;                 // 1 - fstop (the albedo weight's divisor, ARTES.f90:804)
     double* __restrict__ det;       // [NCOPY][4][4][ny][nx]
     size_t det_stride;              // doubles per copy
     double* __restrict__ tot2;      // [6] packet-level sum T^2 per Stokes, flux_emitted, flux_exit

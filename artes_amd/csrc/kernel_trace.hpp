@@ -113,6 +113,10 @@ __device__ __forceinline__ double min_nonan(double a, double b) {
 
 constexpr double INF = __builtin_inf();
 
+// the scaled squared length of a direction's xy part (one expression for every caller, so
+// a constant computed once rounds as the per-trace one would)
+__device__ __forceinline__ double dir_axy(double ax2, double by2, double d0, double d1) { return ax2 * d0 * d0 + by2 * d1 * d1; }
+
 // ------------------------------------------------------- family evaluation ---
 // Nearest crossing ahead among the inner and outer face of ONE coordinate family of cell
 // (cr, ct, cp) from (x, y, z) along n, for a packet sitting on face (ft, fi):
@@ -362,6 +366,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     bool have = false;
 #ifdef ARTES_DEBUG_LANES
     unsigned long long dbg_steps = 0, dbg_lanes = 0, dbg_refills = 0, dbg_tsteps = 0, dbg_tlanes = 0;
+    unsigned long long dbg_anystop = 0, dbg_anyhit = 0, dbg_nstop = 0, dbg_nmove = 0;
 #endif
     // packet state (slot line 0) and trace state
     int slot = -1, mode = 0, pcell = 0, pface = 0, ncross = 0;
@@ -391,11 +396,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     int tsteps = 0;   // steps of the current trace (runaway guard)
     int parked = 0;   // 1: waiting for the batched forced first interaction (3: after a cell error)
 
-    // per-trace constants of the direction, and a fresh family cache
+    // a new direction with its per-trace constants, and a fresh family cache
+    const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
     auto set_direction = [&](double d0, double d1, double d2) {
         nx = d0; ny = d1; nz = d2;
-        const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
-        Axy = ax2 * nx * nx + by2 * ny * ny;
+        Axy = dir_axy(ax2, by2, nx, ny);
         Az = cz2 * nz * nz;
         tacc = 0.0;
         tsteps = 0;
@@ -403,6 +408,27 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         sides = 0;
         e0 = INF; e1 = INF; e2 = INF;
         if constexpr (G3D) inz = fast_rcp(nz);
+    };
+    // every peel-off trace runs along the detector direction: its constants once (3D
+    // grids; radial-only grids recompute them, registers for a 5th wave)
+    double det_Axy = 0.0, det_Az = 0.0, det_inz = 0.0;
+    if constexpr (G3D) {
+        det_Axy = dir_axy(ax2, by2, R.det0, R.det1);
+        det_Az = cz2 * R.det2 * R.det2;
+        det_inz = fast_rcp(R.det2);
+    }
+    auto set_direction_det = [&]() {
+        if constexpr (G3D) {
+            nx = R.det0; ny = R.det1; nz = R.det2;
+            Axy = det_Axy; Az = det_Az; inz = det_inz;
+            tacc = 0.0;
+            tsteps = 0;
+            pending = fam_all;
+            sides = 0;
+            e0 = INF; e1 = INF; e2 = INF;
+        } else {
+            set_direction(R.det0, R.det1, R.det2);
+        }
     };
     // a trace starts at the packet position with zero optical depth
     auto start_trace = [&](double d0, double d1, double d2) {
@@ -446,8 +472,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         }
     };
 
-    // watchdog: a wave runs ~1e5 iterations per launch at the largest pool; a schedule bug
-    // must not leave waves spinning on the device (the run then fails with error 62)
+    // watchdog: a wave runs ~1e4 iterations per launch at the largest pool; a schedule bug
+    // must not leave waves spinning on the device (the run then fails with error 57)
     unsigned int iters = 0;
     for (;;) {
         if (++iters > (1u << 24)) {
@@ -508,6 +534,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         if (cur.exhausted) { dbg_tsteps++; dbg_tlanes += __popcll(__ballot(have)); }
 #endif
         int end = 0;   // 0: continue, else the slot's new mode
+#ifdef ARTES_DEBUG_LANES
+        bool dbg_s = false, dbg_h = false, dbg_m = false;
+#endif
         if (have && !parked) {
             const double k = kext;
             // ------------------------------------------- evaluate one face family
@@ -590,6 +619,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 const bool prop = (mode == S_PROP);
                 const bool hit = prop && tacc + tau_cell > ttgt;
                 const bool stop = err || exit || surf || hit;
+#ifdef ARTES_DEBUG_LANES
+                dbg_s = stop; dbg_h = prop && hit && !err; dbg_m = !stop;
+#endif
                 if constexpr (FLOW) {
                     if (prop && !err && !hit) {   // the segment to the face (ARTES.f90:728-743, 889-904)
                         const int lat = w == 0 ? (side ? 0 : 1) : (w == 1 ? (side ? 2 : 3) : -1);
@@ -619,7 +651,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     px = tx + s * nx; py = ty + s * ny; pz = tz + s * nz;
 #ifdef ARTES_DEBUG_GEOM
                     {   // diagnostic build: is the interaction point in the cell's radial shell?
-                        const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
                         const double S2 = ax2 * px * px + by2 * py * py + cz2 * pz * pz;
                         if (S2 < G.rf2[tcr] * (1 - 1e-9) || S2 > G.rf2[tcr + 1] * (1 + 1e-9)) {
                             if (atomicAdd(&R.err[ARTES_ERR_GEOM], 1ULL) < 6)
@@ -639,14 +670,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     if constexpr (FLOW) flow_segment(R.flow_g, R.flow_t, cell, px, py, pz, nx, ny, nz, s, wI, -1);   // (715, 874)
                     const double xi = rng.uni();   // a killed packet's RNG state is not used again
                     bool kill = !R.photon_scattering || xi < R.fstop;
-                    if (alb < 1.0 && alb > 0.0) wI *= alb / (1.0 - R.fstop);
+                    if (alb < 1.0 && alb > 0.0) wI *= alb / R.omfstop;
                     kill = kill || wI <= R.pmin;
                     if (kill) {
                         end = S_END_ABS;
                     } else {                                       // peel-off trace (ARTES.f90:4722-4761)
+                        // from the interaction point: same cell (kext, alb stay), no face
                         c_peel++;
                         mode = S_PEEL;
-                        start_trace(R.det0, R.det1, R.det2);
+                        tx = px; ty = py; tz = pz;
+                        tft = 0; tfi = 0;
+                        set_direction_det();
                     }
                 } else if (prop) {
                     if (err) {
@@ -699,6 +733,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }   // pending == 0
         }   // have
+#ifdef ARTES_DEBUG_LANES
+        {
+            const unsigned long long bs = __ballot(dbg_s), bh = __ballot(dbg_h), bm = __ballot(dbg_m);
+            dbg_anystop += bs != 0; dbg_anyhit += bh != 0; dbg_nstop += __popcll(bs); dbg_nmove += __popcll(bm);
+        }
+#endif
         q_event.push(end && to_event_list(end), slot, L.event, L.event_n);
         q_emit.push(end && !to_event_list(end), slot, L.emit, L.emit_n);
     }
@@ -706,12 +746,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     q_emit.flush(L.emit, L.emit_n);
 #ifdef ARTES_DEBUG_LANES
     if ((threadIdx.x & 63) == 0) {
-        // (error slots no reference error uses: 0, 30, 32, 40, 41)
+        // (development build: error slots reused as counters, the run's error codes are void)
         atomicAdd(&R.err[0], dbg_steps);
         atomicAdd(&R.err[30], dbg_lanes);
         atomicAdd(&R.err[32], dbg_refills);
         atomicAdd(&R.err[40], dbg_tsteps);
         atomicAdd(&R.err[41], dbg_tlanes);
+        atomicAdd(&R.err[48], dbg_anystop);
+        atomicAdd(&R.err[61], dbg_anyhit);
+        atomicAdd(&R.err[1], dbg_nstop);
+        atomicAdd(&R.err[2], dbg_nmove);
     }
 #endif
     const unsigned long long wv = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);

@@ -572,6 +572,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     if (R.det_phi < 0.0) R.det_phi += 2.0 * M_PI;
     if (R.det_phi > 2.0 * M_PI) R.det_phi -= 2.0 * M_PI;
     R.x_max = p->x_max; R.y_max = p->y_max; R.fstop = p->fstop; R.pmin = p->photon_minimum;
+    R.omfstop = 1.0 - p->fstop;
     R.surface_albedo = p->surface_albedo; R.theta_star = p->theta_star; R.phi_star = p->phi_star;
     R.det = g->d_copies; R.det_stride = stride;
     R.tot2 = tot_out; R.cnt = cnt_out; R.err = err_out; R.rec = rec;
