@@ -66,16 +66,24 @@ __device__ __forceinline__ double fast_sqrt(double x) {
 // The spheres and the theta cones are one quadric form along the ray,
 //     ax2 x^2 + by2 y^2 + w cz2 z^2 - off = 0,
 // with (w, off) = (1, rfront^2) for a radial face and (-tan^2(theta_f), 0) for a theta
-// face (ARTES.f90:2885-3010, 3014-3290).  A face record is {w, off, s, pl}: s is the
+// face (ARTES.f90:2885-3010, 3014-3290).  A face record is {w, off, s, flags}: s is the
 // cone's nappe sign (+1: theta_f > 90 deg, a root with z > 0 is on the other nappe;
-// -1: theta_f < 90 deg, z < 0 is; 0: radial faces and the 90-degree plane) and pl = 1
-// marks the 90-degree plane (tplane = 2).  The records of the radial faces 0..nr are
-// followed by those of the theta faces 0..ntheta, so every family reads its two faces
-// with the same instructions and no per-lane select of coefficients or flags (the phi
-// family reads radial records, whose s and pl are 0); phsc[k] = (sin, cos)(phi_k).
+// -1: theta_f < 90 deg, z < 0 is; 0: radial faces and the 90-degree plane); the flags
+// hold the face's rules as bits, read instead of derived per lane (FR_*): the 90-degree
+// plane (tplane = 2); the same-face veto when the packet sits on the face and it is the
+// cell's outer (KS_OUT) or inner (KS_IN) face -- a sphere only as the inner face
+// (ARTES.f90:2899-2960), a cone when it is the plane or the packet is on the far side of
+// its apex (3014-3290); the grid's polar theta faces, never crossed (EDGE); the 1e-3 m
+// same-face tolerance as outer / inner face (a sphere only as the outer face, a cone
+// both; 2944, 3157).  The records of the radial faces 0..nr are followed by those of the
+// theta faces 0..ntheta, so every family reads its faces with the same instructions and
+// no per-lane select of coefficients or flags (the phi family reads radial records, and
+// ignores them); phsc[k] = (sin, cos)(phi_k).
 struct alignas(32) FaceRec {
-    double w, off, s, pl;
+    double w, off, s;
+    int flags, pad;
 };
+enum : int { FR_PL = 1, FR_KS_OUT = 2, FR_KS_IN = 4, FR_EDGE = 8, FR_BIG_OUT = 16, FR_BIG_IN = 32 };
 
 struct TraceTabs {
     const FaceRec* fr;
@@ -89,12 +97,14 @@ __host__ __device__ inline size_t trace_table_bytes(int nr, int ntheta, int nphi
 __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double* lds) {
     TraceTabs T;
     FaceRec* fr = (FaceRec*)lds;
-    for (int i = threadIdx.x; i <= G.nr; i += BLOCK) fr[i] = FaceRec{1.0, G.rf2[i], 0.0, 0.0};
+    for (int i = threadIdx.x; i <= G.nr; i += BLOCK) fr[i] = FaceRec{1.0, G.rf2[i], 0.0, FR_KS_IN | FR_BIG_OUT, 0};
     for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) {
         const double th = G.thetaf[i];
         const bool cone = G.tplane[i] == 1;
-        fr[G.nr + 1 + i] = FaceRec{-G.tan2[i], 0.0, cone ? (th > HALF_PI ? 1.0 : (th < HALF_PI ? -1.0 : 0.0)) : 0.0,
-                                   cone ? 0.0 : 1.0};
+        const double sg = cone ? (th > HALF_PI ? 1.0 : (th < HALF_PI ? -1.0 : 0.0)) : 0.0;
+        const int fl = (cone ? 0 : FR_PL) | ((!cone || !(sg < 0.0)) ? FR_KS_OUT : 0) | ((!cone || !(sg > 0.0)) ? FR_KS_IN : 0) |
+                       ((i == 0 || i == G.ntheta) ? FR_EDGE : 0) | FR_BIG_OUT | FR_BIG_IN;
+        fr[G.nr + 1 + i] = FaceRec{-G.tan2[i], 0.0, sg, fl, 0};
     }
     double2* phsc = (double2*)(fr + (G.nr + 1) + (G.ntheta + 1));
     for (int i = threadIdx.x; i < G.nphi; i += BLOCK) phsc[i] = make_double2(G.phis[i], G.phic[i]);
@@ -103,8 +113,9 @@ __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double
     return T;
 }
 
-// min of two doubles that are never NaN (roots, or the +inf "no candidate"): one v_min_f64,
-// without the canonicalising v_max the IEEE-mode fmin needs on unknown operands
+// min of two doubles, one v_min_f64 without the canonicalising v_max the IEEE-mode fmin
+// needs on unknown operands.  A quiet-NaN operand (or_nan below: "no crossing") yields the
+// other operand (IEEE minNum); two NaNs yield a NaN.
 __device__ __forceinline__ double min_nonan(double a, double b) {
     double r;
     asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -112,6 +123,13 @@ __device__ __forceinline__ double min_nonan(double a, double b) {
 }
 
 constexpr double INF = __builtin_inf();
+
+// x if valid, else a NaN: only the high word is selected (one v_cndmask instead of two
+// for a double select).  min_nonan ignores the NaN, and every compare with it is false, so
+// a NaN distance means "no crossing" as +inf does.
+__device__ __forceinline__ double or_nan(bool valid, double x) {
+    return __hiloint2double(valid ? __double2hiint(x) : 0x7FF80000, __double2loint(x));
+}
 
 // the scaled squared length of a direction's xy part (one expression for every caller, so
 // a constant computed once rounds as the per-trace one would)
@@ -178,7 +196,7 @@ __device__ __forceinline__ double family_eval(const DevGrid& G, const TraceTabs&
     const int kin_f = isP ? cp : kin, kout_f = isP ? pout : kout;
     const bool onfam = ft == fam + 1;
     const bool same0 = onfam & (fi == kin_f), same1 = onfam & (fi == kout_f);
-    const bool plane0 = G3D && fin.pl != 0.0, plane1 = G3D && fout.pl != 0.0;   // (theta lanes only)
+    const bool plane0 = G3D && (fin.flags & FR_PL), plane1 = G3D && (fout.flags & FR_PL);   // (theta lanes only)
     // existence: the divisor, and for the quadratic the discriminant
     const bool d_ok0 = isP | (disc0 >= 0.0), d_ok1 = isP | (disc1 >= 0.0);
     bool va0 = d_ok0 & (fabs(da0) > 1.e-100);
@@ -245,7 +263,6 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
                                                double n0, double n1, double n2, double Axy, double Az, int ft, int fi,
                                                int cr, int ct, int cp, int pout, double zp, bool alt, bool& outer) {
     const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
-    const bool isR = !G3D || fam == 0;
     const bool isT = G3D && fam == 1;
     const bool isP = G3D && fam == 2;
     const double Bxy = ax2 * x * n0 + by2 * y * n1, Bz = cz2 * z * n2;
@@ -265,7 +282,8 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     }
     const FaceRec fc = T.fr[e + (ch ? 1 : 0)];
     const double w = G3D ? fc.w : 1.0, sg = G3D ? fc.s : 0.0;
-    const bool pl = G3D && fc.pl != 0.0;
+    const int fl = G3D ? fc.flags : (FR_KS_IN | FR_BIG_OUT);
+    const bool pl = G3D && (fl & FR_PL);
     const double qa = fma(w, Az, Axy), qb = 2.0 * fma(w, Bz, Bxy), qc = fma(w, Cz, Cxy) - fc.off;
     const double disc = qb * qb - 4.0 * qa * qc;
     const double q = -0.5 * (qb + copysign(fast_sqrt(disc), qb));
@@ -280,7 +298,6 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     const double dA = isP ? den0 : qa, dB = isP ? den1 : q;
     const double rA = fast_div(isP ? num0 : q, dA);
     const double rB = fast_div(isP ? num1 : qc, dB);
-    const bool fA = !isP & ch, fB = isP | ch;                   // faces of the roots (1: outer)
     const int kA = isP ? cp : kin + (ch ? 1 : 0), kB = isP ? pout : kA;
     const bool sameA = onfam & (fi == kA), sameB = onfam & (fi == kB);
     // existence: the divisor, and for the quadratic the discriminant
@@ -295,22 +312,24 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     // tolerances (1e-3 m to re-cross the face the packet sits on: spheres outer face only,
     // cones both; ARTES.f90:2944, 3157); the 90-degree plane: one root at zp, valid when
     // moving towards it (3066-3070, 3116-3118)
+    // (the chosen face's rules as outer (ch) or inner face: flag bits 1 / 2 and 4 / 5; a
+    // quadratic's two roots are on one face, so they share them)
+    const int fsh = ch ? 0 : 1;
     const double A = pl ? zp : rA;
-    const bool bigA = sameA & (isT | (isR & fA)), bigB = sameB & (isT | (isR & fB));
-    vA = (vA & !pl & (A > 1.e-15) & (!bigA | (A > 1.e-3))) | (pl & (ch ? (n2 < -1.e-15) : (n2 > 1.e-15)) & (A > 0.0));
-    vB = vB & !pl & (rB > 1.e-15) & (!bigB | (rB > 1.e-3));
+    const bool big = !isP & sameA & ((fl >> (4 + fsh)) & 1);
+    vA = (vA & !pl & (A > 1.e-15) & (!big | (A > 1.e-3))) | (pl & (ch ? (n2 < -1.e-15) : (n2 > 1.e-15)) & (A > 0.0));
+    vB = vB & !pl & (rB > 1.e-15) & (!big | (rB > 1.e-3));
     // vetoes (ARTES.f90:2899-2960, 3014-3290, 3318, 3346)
-    const bool tkill = ch ? ((kin + 1 == G.ntheta) | (sameA & (pl | !(sg < 0.0)))) : ((kin == 0) | (sameA & (pl | !(sg > 0.0))));
+    const bool qkill = (fl & FR_EDGE) | (sameA & ((fl >> (1 + fsh)) & 1));
     const bool sp0_big = !sameA & (fabs(den0) > 0.0) & !(rA < 1.e100);
-    const bool killA = (isR & sameA & !fA) | (isT & tkill) | (isP & sameA);
-    const bool killB = (isR & sameB & !fB) | (isT & tkill) | (isP & (sameB | sp0_big));
+    const bool killA = isP ? sameA : qkill;
+    const bool killB = isP ? (sameB | sp0_big) : qkill;
     // equal roots of a quadratic give no crossing; the 1e100 cap
     const bool eq = !isP & vA & vB & (A == rB);
     vA = vA & !killA & !eq & (A < 1.e100);
     vB = vB & !killB & !eq & (rB < 1.e100);
-    const double mA = vA ? A : INF, mB = vB ? rB : INF;
-    outer = isP ? (mB < mA) : ch;
-    return min_nonan(mA, mB);
+    outer = isP ? (vB & (!vA | (rB < A))) : ch;
+    return min_nonan(or_nan(vA, A), or_nan(vB, rB));   // NaN: no crossing
 }
 
 // Energy-transport diagnostics of a propagation segment (output:flow_global /
@@ -573,16 +592,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
                 double best;
                 int w = 0;
-                {
-                    const double t0 = e0 > 1.e-9 ? e0 : INF;
+                {   // (NaN: excluded; ties go to the lower family, as the reference's order)
+                    const double t0 = or_nan(e0 > 1.e-9, e0);
                     best = t0;
                     if constexpr (G3D) {
-                        const double t1 = e1 > 1.e-9 ? e1 : INF, t2 = e2 > 1.e-9 ? e2 : INF;
-                        if (t1 < best) { best = t1; w = 1; }
-                        if (t2 < best) { best = t2; w = 2; }
+                        const double t1 = or_nan(e1 > 1.e-9, e1), t2 = or_nan(e2 > 1.e-9, e2);
+                        best = min_nonan(min_nonan(t0, t1), t2);
+                        w = t0 == best ? 0 : (t1 == best ? 1 : 2);
                     }
                 }
-                if (best == INF) {   // rare: nothing beyond 1e-9 m
+                if (!(best < INF)) {   // rare: nothing beyond 1e-9 m
                     best = e0 > 1.e-12 ? e0 : INF;
                     w = 0;
                     if constexpr (G3D) {
