@@ -285,6 +285,8 @@ def main() -> int:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": "k_trace (dominant: cell-boundary tracing)",
+                     "note": "bound: the HBM roofline the contract prices the kernel against (no MFMA work); "
+                             "k_trace itself is VALU-issue bound, see limiter (SQ counters of this build)",
                      "alg_bytes_per_packet": round(trace_bpp, 1), "alg_bytes_per_launch": round(per_launch),
                      "avg_launch_ms": round(avg_ms, 4), "launches": t_n,
                      "traffic_source": traffic_src,
