@@ -385,7 +385,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     bool have = false;
 #ifdef ARTES_DEBUG_LANES
     unsigned long long dbg_steps = 0, dbg_lanes = 0, dbg_refills = 0, dbg_tsteps = 0, dbg_tlanes = 0;
-    unsigned long long dbg_anystop = 0, dbg_anyhit = 0, dbg_nstop = 0, dbg_nmove = 0;
+    unsigned long long dbg_anystop = 0, dbg_anyhit = 0, dbg_nstop = 0, dbg_nmove = 0, dbg_nretry = 0, dbg_nsetup = 0;
 #endif
     // packet state (slot line 0) and trace state
     int slot = -1, mode = 0, pcell = 0, pface = 0, ncross = 0;
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #endif
         int end = 0;   // 0: continue, else the slot's new mode
 #ifdef ARTES_DEBUG_LANES
-        bool dbg_s = false, dbg_h = false, dbg_m = false;
+        bool dbg_s = false, dbg_h = false, dbg_m = false, dbg_r = false, dbg_u = false;
 #endif
         if (have && !parked) {
             const double k = kext;
@@ -587,6 +587,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 sides = (outer ? 1 : 0) | ((retry ? 1 : 0) << 4);
             }
             if (!retry) pending &= pending - 1;
+#ifdef ARTES_DEBUG_LANES
+            dbg_r = retry; dbg_u = !retry && pending != 0;
+#endif
             if (pending == 0) {
                 // ------------------------------------------------ trace step
                 // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
@@ -756,6 +759,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         {
             const unsigned long long bs = __ballot(dbg_s), bh = __ballot(dbg_h), bm = __ballot(dbg_m);
             dbg_anystop += bs != 0; dbg_anyhit += bh != 0; dbg_nstop += __popcll(bs); dbg_nmove += __popcll(bm);
+            dbg_nretry += __popcll(__ballot(dbg_r)); dbg_nsetup += __popcll(__ballot(dbg_u));
         }
 #endif
         q_event.push(end && to_event_list(end), slot, L.event, L.event_n);
@@ -775,6 +779,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         atomicAdd(&R.err[61], dbg_anyhit);
         atomicAdd(&R.err[1], dbg_nstop);
         atomicAdd(&R.err[2], dbg_nmove);
+        atomicAdd(&R.err[4], dbg_nretry);
+        atomicAdd(&R.err[5], dbg_nsetup);
     }
 #endif
     const unsigned long long wv = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);
