@@ -5,7 +5,8 @@
 // execute the union of all lanes' branches, and carrying the whole packet state plus
 // the scattering math in one kernel costs ~300 VGPRs (one wave per SIMD).  Here the
 // packet life is split at its natural seams into three kernels over a pool of P
-// in-flight packets whose state lives in HBM (one 256-byte record per packet, `Slot`):
+// in-flight packets whose state lives in HBM (a 128-byte transport record per packet,
+// `Slot`, and a 128-byte diagnostic one, `SlotDiag`):
 //
 //   k_trace  the hot loop: cell_face steps (ARTES.f90:2800-3470) of every trace --
 //            first optical depth (625-656), propagation (689-778, 848-941) and peel-off
@@ -31,17 +32,18 @@
 
 namespace artes {
 
-// packet-state pool: one 256-byte record per slot (two 128-byte cache lines).  The
-// work lists visit slots in no particular order, so a record layout keeps every access
-// of a lane inside its own lines; a structure-of-arrays pool would touch one line per
-// field per lane.  Line 0 holds the whole transport state: every kernel reads and writes
-// that line only.  Line 1 holds diagnostics -- the packet-level moments (R.moments),
-// the trace records (R.rec) -- and the rare surface-peel angle, so a production run moves
-// one random line per packet access instead of two.  Every trace starts at the packet
-// position (p*, pcell, pface) with zero accumulated optical depth, so no separate trace
-// position is stored.
-struct alignas(256) Slot {
-    // line 0: transport state
+// packet-state pool: two 128-byte records per slot (one cache line each), in two arrays.
+// The work lists visit slots in no particular order, so a record layout keeps every
+// access of a lane inside its own line; a structure-of-arrays pool would touch one line
+// per field per lane.  `Slot` (line 0) holds the whole transport state: every kernel
+// reads and writes that line only.  `SlotDiag` (line 1) holds diagnostics -- the
+// packet-level moments (R.moments), the trace records (R.rec) -- and the rare
+// surface-peel angle, so a production run moves one random line per packet access, and
+// the random accesses span the P x 128 B of the transport array only.  Every trace
+// starts at the packet position (p*, pcell, pface) with zero accumulated optical depth,
+// so no separate trace position is stored.
+struct alignas(128) Slot {
+    // the transport state, one 128-byte line: every kernel reads and writes only this
     double px, py, pz;                  // packet position (last interaction / emission)
     double dx, dy, dz;                  // packet direction
     double ttgt;                        // target optical depth of a propagation trace
@@ -51,7 +53,13 @@ struct alignas(256) Slot {
     double wI;                          // Stokes I including the weights applied in k_trace
     double tpeel;                       // optical depth of the last peel-off trace
     double q1, q2, q3;                  // Stokes Q, U, V per unit I as of the last scattering
-    // line 1: diagnostics and the surface peel
+};
+static_assert(sizeof(Slot) == 128, "the transport state is one cache line");
+
+// the rest of a packet's record, in an array of its own so the transport kernels' random
+// slot accesses span half the address range (fewer address-translation misses):
+// diagnostics and the surface peel
+struct alignas(128) SlotDiag {
     double cos_surf;                    // surface peel: cos(normal, detector) (ARTES.f90:4623)
     double cs0, cs1, cs2, cs3;          // moments: running contribution to the current pixel
     double pt0, pt1, pt2, pt3;          // moments: packet total per Stokes
@@ -61,8 +69,7 @@ struct alignas(256) Slot {
     double peel_pol[3];                 // trace records: peeled -Q, U, V (detector sign, ARTES.f90:4956)
     double spare1;
 };
-static_assert(sizeof(Slot) == 256, "slot record must be two cache lines");
-static_assert(offsetof(Slot, cos_surf) == 128, "line 0 must hold the whole transport state");
+static_assert(sizeof(SlotDiag) == 128, "one line");
 
 // line 0 of a slot as k_event reads it (loaded one event ahead, see k_event)
 struct alignas(16) Line0 {
@@ -76,7 +83,8 @@ static_assert(sizeof(Line0) == 128 && offsetof(Line0, wI) == offsetof(Slot, wI) 
 
 struct Pool {
     int P;
-    Slot* __restrict__ s;
+    Slot* __restrict__ s;        // [P] transport state
+    SlotDiag* __restrict__ d;    // [P] diagnostics, surface peel
 };
 
 // A trace list is read as list index j < split -> position j, j >= split -> position
@@ -325,20 +333,20 @@ __device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int s
     double* __restrict__ det = D.det;
     const size_t plane = D.plane;
     if (R.moments) {
-        const int cur = S.s[slot].cur_pix;
-        double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
+        const int cur = S.d[slot].cur_pix;
+        double cs[4] = {S.d[slot].cs0, S.d[slot].cs1, S.d[slot].cs2, S.d[slot].cs3};
         if (pix != cur) {
             if (cur >= 0) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
             }
-            S.s[slot].cur_pix = pix;
+            S.d[slot].cur_pix = pix;
             cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
         }
-        S.s[slot].cs0 = cs[0] + v; S.s[slot].cs1 = cs[1]; S.s[slot].cs2 = cs[2]; S.s[slot].cs3 = cs[3];
-        S.s[slot].pt0 += v;
+        S.d[slot].cs0 = cs[0] + v; S.d[slot].cs1 = cs[1]; S.d[slot].cs2 = cs[2]; S.d[slot].cs3 = cs[3];
+        S.d[slot].pt0 += v;
     }
-    if (R.rec) S.s[slot].peel_sum += v;
+    if (R.rec) S.d[slot].peel_sum += v;
     c_det++;
 }
 
@@ -380,7 +388,7 @@ __device__ __forceinline__ int event_surface_hit(const DevGrid& G, const DevRun&
     S.s[slot].q1 = 0.0; S.s[slot].q2 = 0.0; S.s[slot].q3 = 0.0;
     // cos of the angle between the surface normal and the detector (4623-4625)
     const double cos_angle = n0 * R.det0 + n1 * R.det1 + n2 * R.det2;
-    S.s[slot].cos_surf = cos_angle;
+    S.d[slot].cos_surf = cos_angle;
     S.s[slot].mode = cos_angle > 0.0 ? S_PEEL_S : S_PROP;
     return 1;
 }
@@ -391,7 +399,7 @@ __device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S
     const int m = S.s[slot].mode;
     const double tau = S.s[slot].tpeel;
     if (!(m & FLAG_ERR) && (m & FLAG_EXIT) && tau < 50.0)
-        add_peel_I(R, S, slot, D, exp(-tau) * S.s[slot].cos_surf / PI * S.s[slot].wI, 52, c_det);
+        add_peel_I(R, S, slot, D, exp(-tau) * S.d[slot].cos_surf / PI * S.s[slot].wI, 52, c_det);
     S.s[slot].mode = S_PROP;
     return 1;
 }
@@ -475,23 +483,23 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                         }
                         D.add(8, pix, 1.0);
                         if (R.moments) {   // packet-level moments (diagnostics, line 1)
-                            const int cur = S.s[slot].cur_pix;
-                            double cs[4] = {S.s[slot].cs0, S.s[slot].cs1, S.s[slot].cs2, S.s[slot].cs3};
+                            const int cur = S.d[slot].cur_pix;
+                            double cs[4] = {S.d[slot].cs0, S.d[slot].cs1, S.d[slot].cs2, S.d[slot].cs3};
                             if (pix != cur) {
                                 if (cur >= 0) {
 #pragma unroll
                                     for (int q = 0; q < 4; q++) unsafeAtomicAdd(&det[(12 + q) * plane + cur], cs[q] * cs[q]);
                                 }
-                                S.s[slot].cur_pix = pix;
+                                S.d[slot].cur_pix = pix;
                                 cs[0] = cs[1] = cs[2] = cs[3] = 0.0;
                             }
-                            S.s[slot].cs0 = cs[0] + v[0]; S.s[slot].cs1 = cs[1] + v[1];
-                            S.s[slot].cs2 = cs[2] + v[2]; S.s[slot].cs3 = cs[3] + v[3];
-                            S.s[slot].pt0 += v[0]; S.s[slot].pt1 += v[1]; S.s[slot].pt2 += v[2]; S.s[slot].pt3 += v[3];
+                            S.d[slot].cs0 = cs[0] + v[0]; S.d[slot].cs1 = cs[1] + v[1];
+                            S.d[slot].cs2 = cs[2] + v[2]; S.d[slot].cs3 = cs[3] + v[3];
+                            S.d[slot].pt0 += v[0]; S.d[slot].pt1 += v[1]; S.d[slot].pt2 += v[2]; S.d[slot].pt3 += v[3];
                         }
                         if (R.rec) {
-                            S.s[slot].peel_sum += wI;
-                            S.s[slot].peel_pol[0] += v[1]; S.s[slot].peel_pol[1] += v[2]; S.s[slot].peel_pol[2] += v[3];
+                            S.d[slot].peel_sum += wI;
+                            S.d[slot].peel_pol[0] += v[1]; S.d[slot].peel_pol[1] += v[2]; S.d[slot].peel_pol[2] += v[3];
                         }
                         c_det++;
                     }
@@ -503,7 +511,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         if (drop) { S.s[slot].mode = S_END_DROP; return 2; }
         // scatter_photon + polarization_rotation (ARTES.f90:819-846)
         c_scat++;
-        if (R.rec) S.s[slot].nscat += 1;
+        if (R.rec) S.d[slot].nscat += 1;
         Rng rng; rng.s0 = L0.r0; rng.s1 = L0.r1;
         double alpha, beta;
         sample_angles(G, R, G.cums + (size_t)mid * CUM_DOUBLES, rng, st, alpha, beta);
@@ -725,26 +733,26 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
             else if (m == S_END_ABS) c_abs++;
             else c_drop++;
             if (R.moments) {
-                const int cur = S.s[slot].cur_pix;
+                const int cur = S.d[slot].cur_pix;
                 if (cur >= 0) {
-                    unsafeAtomicAdd(&det[12 * plane + cur], S.s[slot].cs0 * S.s[slot].cs0);
-                    unsafeAtomicAdd(&det[13 * plane + cur], S.s[slot].cs1 * S.s[slot].cs1);
-                    unsafeAtomicAdd(&det[14 * plane + cur], S.s[slot].cs2 * S.s[slot].cs2);
-                    unsafeAtomicAdd(&det[15 * plane + cur], S.s[slot].cs3 * S.s[slot].cs3);
+                    unsafeAtomicAdd(&det[12 * plane + cur], S.d[slot].cs0 * S.d[slot].cs0);
+                    unsafeAtomicAdd(&det[13 * plane + cur], S.d[slot].cs1 * S.d[slot].cs1);
+                    unsafeAtomicAdd(&det[14 * plane + cur], S.d[slot].cs2 * S.d[slot].cs2);
+                    unsafeAtomicAdd(&det[15 * plane + cur], S.d[slot].cs3 * S.d[slot].cs3);
                 }
-                const double a0 = S.s[slot].pt0, a1 = S.s[slot].pt1, a2 = S.s[slot].pt2, a3 = S.s[slot].pt3;
+                const double a0 = S.d[slot].pt0, a1 = S.d[slot].pt1, a2 = S.d[slot].pt2, a3 = S.d[slot].pt3;
                 t2[0] += a0 * a0; t2[1] += a1 * a1; t2[2] += a2 * a2; t2[3] += a3 * a3;
             }
             if (m == S_END_EXIT && R.photon_source == 2) f_exit += S.s[slot].wI;
             if constexpr (TRACE) {
-                double* rr = R.rec + (size_t)(S.s[slot].pid - R.first) * ARTES_TRACE_FIELDS;
-                rr[0] = S.s[slot].peel_sum;
-                rr[1] = (double)S.s[slot].nscat;
+                double* rr = R.rec + (size_t)(S.d[slot].pid - R.first) * ARTES_TRACE_FIELDS;
+                rr[0] = S.d[slot].peel_sum;
+                rr[1] = (double)S.d[slot].nscat;
                 rr[2] = (double)S.s[slot].ncross;
                 rr[3] = (double)(m - S_END_EXIT + 1);   // 1 exit, 2 absorbed, 3 dropped
-                rr[4] = S.s[slot].peel_pol[0];
-                rr[5] = S.s[slot].peel_pol[1];
-                rr[6] = S.s[slot].peel_pol[2];
+                rr[4] = S.d[slot].peel_pol[0];
+                rr[5] = S.d[slot].peel_pol[1];
+                rr[6] = S.d[slot].peel_pol[2];
                 rr[7] = 0.0;
             }
         }
@@ -814,15 +822,15 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
         S.s[slot].ncross = 0;
         S.s[slot].mode = mode0;
         if (R.moments) {
-            S.s[slot].cs0 = S.s[slot].cs1 = S.s[slot].cs2 = S.s[slot].cs3 = 0.0;
-            S.s[slot].pt0 = S.s[slot].pt1 = S.s[slot].pt2 = S.s[slot].pt3 = 0.0;
-            S.s[slot].cur_pix = -1;
+            S.d[slot].cs0 = S.d[slot].cs1 = S.d[slot].cs2 = S.d[slot].cs3 = 0.0;
+            S.d[slot].pt0 = S.d[slot].pt1 = S.d[slot].pt2 = S.d[slot].pt3 = 0.0;
+            S.d[slot].cur_pix = -1;
         }
         if constexpr (TRACE) {
-            S.s[slot].pid = pid;
-            S.s[slot].peel_sum = 0.0;
-            S.s[slot].peel_pol[0] = S.s[slot].peel_pol[1] = S.s[slot].peel_pol[2] = 0.0;
-            S.s[slot].nscat = 0;
+            S.d[slot].pid = pid;
+            S.d[slot].peel_sum = 0.0;
+            S.d[slot].peel_pol[0] = S.d[slot].peel_pol[1] = S.d[slot].peel_pol[2] = 0.0;
+            S.d[slot].nscat = 0;
         }
         }   // emit
         if (i < n) L.trace_out[out0 + i] = emit ? slot : -1;

@@ -1,8 +1,8 @@
 // transport.hip -- MI355X (gfx950) photon-packet transport engine + C ABI.
 //
 // The hot path of the reference, `radiative_transfer` (ARTES.f90:518-1006), runs here as
-// an EVENT ENGINE over a pool of in-flight packets in HBM (one 256-byte record per slot,
-// kernel_event.hpp): one host iteration launches
+// an EVENT ENGINE over a pool of in-flight packets in HBM (a 128-byte transport record
+// and a 128-byte diagnostic record per slot, kernel_event.hpp): one host iteration launches
 //   k_trace  (kernel_trace.hpp) every cell_face step (ARTES.f90:2800-3470) of the first
 //            optical depth, propagation and peel-off traces, one packet per lane, lanes
 //            refilling themselves from the trace list;
@@ -282,19 +282,22 @@ static bool use_event_engine() {
     return !(e && std::string(e) == "persistent");
 }
 
-// allocate the packet pool (256-byte slot records) and the work lists of the event engine
+// allocate the packet pool (transport and diagnostic records) and the work lists of the
+// event engine
 static int32_t ensure_pool(artes_grid* g) {
     if (g->pool_mem) return 0;
     const char* env = getenv("ARTES_POOL");
-    // 64 Ki slots per CU (16.8 M, 4.3 GB on MI355X): every k_trace launch ends in a tail of
-    // a few long traces (~0.45 ms), so fewer, larger iterations pay it less often; beyond
-    // this the random slot accesses of k_event start to miss in the TLBs (pool sweep in
-    // DESIGN.md §3)
-    long long P = env ? atoll(env) : (long long)g->num_cus * 65536;
+    // 96 Ki slots per CU (25.2 M on MI355X; 3.2 GB of transport records + 3.2 GB of
+    // diagnostic ones): every k_trace launch ends in a tail of a few long traces
+    // (~0.35 ms), so fewer, larger iterations pay it less often; past ~30 M slots the
+    // random transport-record accesses of k_event and k_emit start to miss in the TLBs
+    // (pool sweep in DESIGN.md §3)
+    long long P = env ? atoll(env) : (long long)g->num_cus * 98304;
     P = std::max<long long>(1024, std::min<long long>(P, 1LL << 26));
-    HIP_TRY(hipMalloc(&g->pool_mem, (size_t)P * sizeof(Slot)));
+    HIP_TRY(hipMalloc(&g->pool_mem, (size_t)P * (sizeof(Slot) + sizeof(SlotDiag))));
     g->pool.P = (int)P;
     g->pool.s = (Slot*)g->pool_mem;
+    g->pool.d = (SlotDiag*)((char*)g->pool_mem + (size_t)P * sizeof(Slot));
     HIP_TRY(hipMalloc((void**)&g->d_lists[0], (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_lists[1], (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_event, (size_t)P * 4));
@@ -351,10 +354,12 @@ static void dump_live(artes_grid* g, const int* d_n, const int* d_list, const in
         const int pos = j < split ? j : P - 1 - (j - split);
         int slot = -1;
         Slot r;
+        SlotDiag q;
         if (hipMemcpy(&slot, d_list + pos, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || slot < 0 || slot >= P) continue;
         if (hipMemcpy(&r, g->pool.s + slot, sizeof(Slot), hipMemcpyDeviceToHost) != hipSuccess) continue;
+        if (hipMemcpy(&q, g->pool.d + slot, sizeof(SlotDiag), hipMemcpyDeviceToHost) != hipSuccess) continue;
         fprintf(stderr, "[artes] slot %d pid %llu mode %d p %.17g %.17g %.17g d %.17g %.17g %.17g ttgt %.17g cell %d face %d ncross %d nscat %d wI %.17g\n",
-                slot, r.pid, r.mode, r.px, r.py, r.pz, r.dx, r.dy, r.dz, r.ttgt, r.pcell, r.pface, r.ncross, r.nscat, r.wI);
+                slot, q.pid, r.mode, r.px, r.py, r.pz, r.dx, r.dy, r.dz, r.ttgt, r.pcell, r.pface, r.ncross, q.nscat, r.wI);
     }
 }
 
