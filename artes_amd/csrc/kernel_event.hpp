@@ -102,7 +102,24 @@ struct Lists {
     unsigned long long* next_pkt;       // packets handed out so far
     int* dbg_owner;                     // ARTES_DEBUG: [P] last (iteration, stage) tag per slot
     int* dbg_iter;                      // ARTES_DEBUG: iteration counter (k_rotate)
+    int P;                              // list capacity: the slots of this sub-engine
+    unsigned long long first, n;        // the packet ids of this sub-engine: [first, first + n)
 };
+
+// XCD-partitioned sub-engines.  MI355X dispatches the blocks of a grid round-robin over
+// its 8 XCDs, each with its own L2 and address-translation caches.  The pool is split
+// into NSUB parts of P / NSUB slots with lists, counters and packet ids of their own, and
+// the blocks b of every kernel with b % NSUB == s work on part s only (block b / NSUB of
+// the part's b' grid): a slot stays on one XCD for its whole life, and an XCD's random
+// record accesses span 1/8 of the pool.  The packet ids [first, first + n) are split into
+// NSUB contiguous ranges; results per packet id are unchanged.
+constexpr int NSUB = 8;
+struct SubLists {
+    Lists l[NSUB];
+};
+__device__ __forceinline__ int sub_of_block() { return (int)blockIdx.x % NSUB; }
+__device__ __forceinline__ int sub_block() { return (int)blockIdx.x / NSUB; }
+__device__ __forceinline__ int sub_grid() { return (int)gridDim.x / NSUB; }
 
 // Work-list invariants of one engine iteration (checked by ARTES_DEBUG builds; a
 // violation counts error ARTES_ERR_LISTS and fails the run):
@@ -173,8 +190,8 @@ struct TraceCursor {
 };
 
 __device__ __forceinline__ TraceCursor make_cursor(int n, int static_q64) {
-    const int W = (int)gridDim.x * (BLOCK / 64);
-    const int w = (int)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+    const int W = sub_grid() * (BLOCK / 64);            // the waves of this sub-engine
+    const int w = sub_block() * (BLOCK / 64) + (threadIdx.x >> 6);
     const int nchunk = (int)((((long long)n * static_q64) >> 6) >> 6);
     TraceCursor c;
     c.chunk = w;
@@ -559,8 +576,9 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
 //  PIX1:  a one-pixel detector: per-lane register sums, reduced over the wave at the end
 //         (DetAcc); no LDS detector then.
 template <bool LDS_T, bool LDS_D, bool PIX1 = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, Lists L) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, SubLists SL) {
     static_assert(!(PIX1 && LDS_D), "a one-pixel detector is reduced in registers");
+    const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_ev[];
     DevGrid G = G0;
     const size_t plane = (size_t)R.nx * R.ny;
@@ -592,8 +610,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
     // Software pipeline: the slot ids come two events ahead and line 0 of the next event's
     // record one event ahead, so the record loads (random lines in the pool) overlap the
     // current event's arithmetic instead of stalling at its start.
-    const int stride = (int)gridDim.x * BLOCK;
-    int i = blockIdx.x * BLOCK + threadIdx.x;
+    const int stride = sub_grid() * BLOCK;
+    int i = sub_block() * BLOCK + threadIdx.x;
     int slot = i < n ? L.event[i] : -1;
     int slot_n = i + stride < n ? L.event[i + stride] : -1;
     Line0 cur;
@@ -608,7 +626,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
         const int dest = slot >= 0 ? event_one<PIX1>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
-        if (i < n) L.trace_out[R.emit_first ? S.P - 1 - i : i] = (dest == 1) ? slot : -1;
+        if (i < n) L.trace_out[R.emit_first ? L.P - 1 - i : i] = (dest == 1) ? slot : -1;
         wave_append(dest == 2, slot, L.emit, L.emit_n);
         slot = slot_n;
         slot_n = slot_nn;
@@ -703,7 +721,8 @@ __device__ __forceinline__ int face_interval(const double* f, int n, double v) {
 }
 
 template <bool G3D, bool TRACE>
-__global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lists L) {
+__global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, SubLists SL) {
+    const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_em[];
     double* s_tf = s_em;                      // theta faces
     double* s_pf = s_em + (G.ntheta + 1);     // phi faces, then 2 pi
@@ -722,7 +741,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
     double t2[4] = {0, 0, 0, 0};
     double f_emit = 0.0, f_exit = 0.0;   // thermal flux_emitted / flux_exit (ARTES.f90:607, 780, 953)
     const int n_pad = (n + 63) & ~63;
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n_pad; i += gridDim.x * BLOCK) {
+    for (int i = sub_block() * BLOCK + threadIdx.x; i < n_pad; i += sub_grid() * BLOCK) {
         const int slot = i < n ? L.emit[i] : -1;
         const int m = slot >= 0 ? S.s[slot].mode : S_RETIRED;
 #ifdef ARTES_DEBUG
@@ -757,11 +776,11 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
             }
         }
         const unsigned long long k = pkt0 + (unsigned long long)i;
-        const bool emit = slot >= 0 && k < R.n;
+        const bool emit = slot >= 0 && k < L.n;
         if (slot >= 0 && !emit) S.s[slot].mode = S_RETIRED;
         if (emit) {
         c_pkt++;
-        const unsigned long long pid = R.first + k;
+        const unsigned long long pid = L.first + k;
         Rng rng;
         rng.seed(R.seed, pid);
         double px, py, pz, dx, dy, dz, wI = 1.0;
@@ -859,20 +878,38 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Lis
 
 // initial fill: the first `use` slots are fresh and queued for emission (a run of fewer
 // packets than the pool holds leaves the rest untouched: no list ever names them)
-__global__ void k_init(Pool S, int* emit, int* emit_n, int use) {
+// the first `use[s]` slots of every sub-engine s are free and queued for emission
+struct SubUse {
+    int u[NSUB];
+};
+__global__ void k_init(Pool S, int* emit, int* emit_n /*[NSUB]*/, int Ps, SubUse use) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < use) {
+    if (i >= Ps * NSUB) return;
+    const int sub = i / Ps, j = i - sub * Ps;
+    if (j < use.u[sub]) {
         S.s[i].mode = S_FRESH;
-        emit[i] = i;
+        emit[i] = i;   // position j of sub-engine sub's emit list
     }
-    if (i == 0) *emit_n = use;
+    if (j == 0) emit_n[sub] = use.u[sub];
 }
 
 // end of an iteration: the output trace list (k_event's event_n entries, then k_emit's
 // emit_n) becomes the input, the consumed input buffer is reset to become the next
 // output, packet ids advance by the emit-list length; event/emit lists and cursors are zeroed
-__global__ void k_rotate(int* in_n, int* out_n, int* out_split, int* event_n, int* emit_n, unsigned int* grab,
-                         unsigned long long* next_pkt, int emit_first, int P, int* dbg_iter, unsigned long long* err) {
+// (one block per sub-engine; counters are laid out [field][NSUB], see CNT_*)
+enum : int { CNT_IN0 = 0, CNT_IN1 = 1, CNT_EVENT = 2, CNT_EMIT = 3, CNT_SPLIT0 = 4, CNT_SPLIT1 = 5, CNT_DBG = 8, CNT_FIELDS = 16 };
+__global__ void k_rotate(int* cnt, int in, unsigned int* grab_all, unsigned long long* next_all, int emit_first, int P,
+                         unsigned long long* err) {
+    const int sub = blockIdx.x;
+    int* in_n = cnt + (CNT_IN0 + in) * NSUB + sub;
+    int* out_n = cnt + (CNT_IN0 + 1 - in) * NSUB + sub;
+    int* out_split = cnt + (CNT_SPLIT0 + 1 - in) * NSUB + sub;
+    int* event_n = cnt + CNT_EVENT * NSUB + sub;
+    int* emit_n = cnt + CNT_EMIT * NSUB + sub;
+    int* dbg_iter = cnt + CNT_DBG * NSUB + sub;
+    unsigned int* grab = grab_all + 8 * sub;
+    unsigned long long* next_pkt = next_all + sub;
+    (void)dbg_iter; (void)err;
     if (threadIdx.x == 0) {
         const int ev = *event_n, em = *emit_n;
 #ifdef ARTES_DEBUG

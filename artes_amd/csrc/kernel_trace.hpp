@@ -370,12 +370,13 @@ __device__ __noinline__ void flow_segment(double* flow_g, double* flow_t, int ce
 //
 // FLOW instantiations add the energy-transport diagnostics to propagation segments.
 template <bool G3D, bool OBL, int WPE, bool FLOW = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G, DevRun R, Pool S, Lists L) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G, DevRun R, Pool S, SubLists SL) {
+    const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_tab[];
     const TraceTabs T = stage_trace_tables(G, s_tab);
     const int n = *L.trace_in_n;
     const int split = *L.trace_in_split;   // [0, split): new packets' traces; then k_event's, stored backwards
-    const int home = blockIdx.x & 7;
+    const int home = sub_block() & 7;
     __shared__ int s_q[2][BLOCK];
     const int wbase = threadIdx.x & ~63;
     WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
@@ -521,12 +522,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
                 dbg_refills++;
 #endif
-                if (!have && my >= 0) slot = L.trace_in[my < split ? my : S.P - 1 - (my - split)];
+                if (!have && my >= 0) slot = L.trace_in[my < split ? my : L.P - 1 - (my - split)];
 #ifdef ARTES_DEBUG
                 if (!have && my >= 0) {
-                    const int pos = my < split ? my : S.P - 1 - (my - split);
+                    const int pos = my < split ? my : L.P - 1 - (my - split);
                     const int m = (slot >= 0 && slot < S.P) ? S.s[slot].mode : S_FIRST;
-                    dbg_claim(R, L, (my < n && pos >= 0 && pos < S.P) ? slot : -2, S.P, 0, m == S_FIRST || m == S_PROP || is_peel_trace(m));
+                    dbg_claim(R, L, (my < n && pos >= 0 && pos < L.P) ? slot : -2, S.P, 0, m == S_FIRST || m == S_PROP || is_peel_trace(m));
                 }
 #endif
                 if (!have && my >= 0 && slot >= 0) {   // -1: a hole left by a dropped or retired packet

@@ -287,13 +287,15 @@ static bool use_event_engine() {
 static int32_t ensure_pool(artes_grid* g) {
     if (g->pool_mem) return 0;
     const char* env = getenv("ARTES_POOL");
-    // 96 Ki slots per CU (25.2 M on MI355X; 3.2 GB of transport records + 3.2 GB of
+    // 128 Ki slots per CU (33.6 M on MI355X; 4.3 GB of transport records + 4.3 GB of
     // diagnostic ones): every k_trace launch ends in a tail of a few long traces
-    // (~0.35 ms), so fewer, larger iterations pay it less often; past ~30 M slots the
-    // random transport-record accesses of k_event and k_emit start to miss in the TLBs
-    // (pool sweep in DESIGN.md §3)
-    long long P = env ? atoll(env) : (long long)g->num_cus * 98304;
+    // (~0.35 ms), so fewer, larger iterations pay it less often.  With one pool the random
+    // record accesses of k_event and k_emit missed in the TLBs past ~30 M slots; split
+    // over the XCDs (NSUB sub-engines) they no longer do up to 50 M (pool sweep in
+    // DESIGN.md §3)
+    long long P = env ? atoll(env) : (long long)g->num_cus * 131072;
     P = std::max<long long>(1024, std::min<long long>(P, 1LL << 26));
+    P -= P % (64 * NSUB);   // NSUB sub-engines of whole waves of slots
     HIP_TRY(hipMalloc(&g->pool_mem, (size_t)P * (sizeof(Slot) + sizeof(SlotDiag))));
     g->pool.P = (int)P;
     g->pool.s = (Slot*)g->pool_mem;
@@ -302,9 +304,9 @@ static int32_t ensure_pool(artes_grid* g) {
     HIP_TRY(hipMalloc((void**)&g->d_lists[1], (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_event, (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_emit, (size_t)P * 4));
-    HIP_TRY(hipMalloc((void**)&g->d_counts, 16 * sizeof(int)));
-    HIP_TRY(hipMalloc((void**)&g->d_grab, 16 * sizeof(unsigned int)));
-    HIP_TRY(hipMalloc((void**)&g->d_next, sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc((void**)&g->d_counts, CNT_FIELDS * NSUB * sizeof(int)));
+    HIP_TRY(hipMalloc((void**)&g->d_grab, 8 * NSUB * sizeof(unsigned int)));
+    HIP_TRY(hipMalloc((void**)&g->d_next, NSUB * sizeof(unsigned long long)));
     HIP_TRY(hipHostMalloc((void**)&g->h_count, 64, hipHostMallocDefault));
 #ifdef ARTES_DEBUG
     HIP_TRY(hipMalloc((void**)&g->d_owner, (size_t)P * sizeof(int)));
@@ -313,12 +315,15 @@ static int32_t ensure_pool(artes_grid* g) {
     return 0;
 }
 
+// grids are whole multiples of the sub-engine count (block b works on sub-engine b % NSUB)
+static int round_sub(int blocks) { return std::max(NSUB, (blocks + NSUB - 1) / NSUB * NSUB); }
+
 // k_trace (kernel_trace.hpp) with its face tables in LDS
 template <bool G3D, bool OBL, int WPE, bool FLOW = false>
-static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const Lists& L, hipStream_t stream) {
+static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L, hipStream_t stream) {
     const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
     const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW>, lds);
-    g->trace_blocks = per_cu * g->num_cus;
+    g->trace_blocks = round_sub(per_cu * g->num_cus);
     timed(g, ARTES_K_TRACE, stream, [&] {
         hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
@@ -327,7 +332,7 @@ static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun&
 // k_trace variant: 3D or radial-only grid, spheroidal (oblate) or spherical planet,
 // occupancy target (waves per SIMD the register budget is sized for)
 template <bool G3D>
-static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, const DevRun& R, const Lists& L,
+static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L,
                              hipStream_t stream) {
     const bool oblate = !(G.ax2 == 1.0 && G.by2 == 1.0 && G.cz2 == 1.0 && G.a == 1.0 && G.b == 1.0);
     if (R.flow_g || R.flow_t) {   // diagnostics: one occupancy target only
@@ -343,23 +348,27 @@ static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, 
 }
 
 // diagnostics (ARTES_VERBOSE) when the engine does not terminate: the transport state of
-// the first packets still in the trace list
-static void dump_live(artes_grid* g, const int* d_n, const int* d_list, const int* d_split, int P, hipStream_t stream) {
-    int n = 0, split = 0;
-    if (hipMemcpyAsync(&n, d_n, sizeof(int), hipMemcpyDeviceToHost, stream) != hipSuccess) return;
-    if (hipMemcpyAsync(&split, d_split, sizeof(int), hipMemcpyDeviceToHost, stream) != hipSuccess) return;
+// the first packets still in the trace lists
+static void dump_live(artes_grid* g, const int* cnt, int in, hipStream_t stream) {
+    const int P = g->pool.P, Ps = P / NSUB;
+    int n[NSUB], split[NSUB];
+    if (hipMemcpyAsync(n, cnt + (CNT_IN0 + in) * NSUB, sizeof(n), hipMemcpyDeviceToHost, stream) != hipSuccess) return;
+    if (hipMemcpyAsync(split, cnt + (CNT_SPLIT0 + in) * NSUB, sizeof(split), hipMemcpyDeviceToHost, stream) != hipSuccess) return;
     if (hipStreamSynchronize(stream) != hipSuccess) return;
-    fprintf(stderr, "[artes] live trace list: %d entries (split %d)\n", n, split);
-    for (int j = 0; j < n && j < 8; j++) {
-        const int pos = j < split ? j : P - 1 - (j - split);
-        int slot = -1;
-        Slot r;
-        SlotDiag q;
-        if (hipMemcpy(&slot, d_list + pos, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || slot < 0 || slot >= P) continue;
-        if (hipMemcpy(&r, g->pool.s + slot, sizeof(Slot), hipMemcpyDeviceToHost) != hipSuccess) continue;
-        if (hipMemcpy(&q, g->pool.d + slot, sizeof(SlotDiag), hipMemcpyDeviceToHost) != hipSuccess) continue;
-        fprintf(stderr, "[artes] slot %d pid %llu mode %d p %.17g %.17g %.17g d %.17g %.17g %.17g ttgt %.17g cell %d face %d ncross %d nscat %d wI %.17g\n",
-                slot, q.pid, r.mode, r.px, r.py, r.pz, r.dx, r.dy, r.dz, r.ttgt, r.pcell, r.pface, r.ncross, q.nscat, r.wI);
+    for (int s = 0; s < NSUB; s++) {
+        fprintf(stderr, "[artes] sub-engine %d: live trace list %d entries (split %d)\n", s, n[s], split[s]);
+        const int* d_list = g->d_lists[in] + (size_t)s * Ps;
+        for (int j = 0; j < n[s] && j < 2; j++) {
+            const int pos = j < split[s] ? j : Ps - 1 - (j - split[s]);
+            int slot = -1;
+            Slot r;
+            SlotDiag q;
+            if (hipMemcpy(&slot, d_list + pos, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || slot < 0 || slot >= P) continue;
+            if (hipMemcpy(&r, g->pool.s + slot, sizeof(Slot), hipMemcpyDeviceToHost) != hipSuccess) continue;
+            if (hipMemcpy(&q, g->pool.d + slot, sizeof(SlotDiag), hipMemcpyDeviceToHost) != hipSuccess) continue;
+            fprintf(stderr, "[artes] slot %d pid %llu mode %d p %.17g %.17g %.17g d %.17g %.17g %.17g ttgt %.17g cell %d face %d ncross %d nscat %d wI %.17g\n",
+                    slot, q.pid, r.mode, r.px, r.py, r.pz, r.dx, r.dy, r.dz, r.ttgt, r.pcell, r.pface, r.ncross, q.nscat, r.wI);
+        }
     }
 }
 
@@ -367,13 +376,13 @@ template <bool G3D>
 static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R, bool trace, hipStream_t stream) {
     int32_t rc = ensure_pool(g);
     if (rc) return rc;
-    const int P = g->pool.P;
-    HIP_TRY(hipMemsetAsync(g->d_counts, 0, 16 * sizeof(int), stream));
-    HIP_TRY(hipMemsetAsync(g->d_grab, 0, 16 * sizeof(unsigned int), stream));
-    HIP_TRY(hipMemsetAsync(g->d_next, 0, sizeof(unsigned long long), stream));
+    const int P = g->pool.P, Ps = P / NSUB;
+    HIP_TRY(hipMemsetAsync(g->d_counts, 0, CNT_FIELDS * NSUB * sizeof(int), stream));
+    HIP_TRY(hipMemsetAsync(g->d_grab, 0, 8 * NSUB * sizeof(unsigned int), stream));
+    HIP_TRY(hipMemsetAsync(g->d_next, 0, NSUB * sizeof(unsigned long long), stream));
     if (g->d_owner) HIP_TRY(hipMemsetAsync(g->d_owner, 0xFF, (size_t)P * sizeof(int), stream));   // tags -1: unclaimed
     int* cnt = g->d_counts;
-    const int side_blocks = std::max(1, g->num_cus * 8);
+    const int side_blocks = round_sub(g->num_cus * 8);
     // launch knobs, read once per call (tuning overrides; the defaults are the measured optima)
     const char* we = getenv("ARTES_WPE");
     const int wpe = we ? atoi(we) : 4;
@@ -401,34 +410,48 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         int per_cu = ev_lds ? blocks_per_cu(g, k_event<true, true>, b) : blocks_per_cu(g, k_event<false, true>, b);
         const char* eb = getenv("ARTES_EVENT_BPC");
         if (eb) per_cu = std::max(1, atoi(eb));
-        ev_blocks = per_cu * g->num_cus;
+        ev_blocks = round_sub(per_cu * g->num_cus);
+    }
+    // the packet ids of the call split into NSUB contiguous ranges, one per sub-engine
+    const uint64_t chunk = (R.n + NSUB - 1) / NSUB;
+    uint64_t sub_first[NSUB], sub_n[NSUB];
+    for (int s = 0; s < NSUB; s++) {
+        const uint64_t lo = std::min<uint64_t>(R.n, (uint64_t)s * chunk), hi = std::min<uint64_t>(R.n, lo + chunk);
+        sub_first[s] = R.first + lo;
+        sub_n[s] = hi - lo;
     }
     auto lists = [&](int in) {
-        Lists L;
-        L.trace_in = g->d_lists[in]; L.trace_in_n = cnt + in; L.trace_in_split = cnt + 4 + in;
-        L.trace_out = g->d_lists[1 - in]; L.trace_out_n = cnt + (1 - in);
-        L.event = g->d_event; L.event_n = cnt + 2;
-        L.emit = g->d_emit; L.emit_n = cnt + 3;
-        L.grab = g->d_grab; L.next_pkt = g->d_next;
-        L.dbg_owner = g->d_owner; L.dbg_iter = cnt + 8;
-        return L;
+        SubLists SL;
+        for (int s = 0; s < NSUB; s++) {
+            Lists& L = SL.l[s];
+            const size_t o = (size_t)s * Ps;
+            L.trace_in = g->d_lists[in] + o; L.trace_in_n = cnt + (CNT_IN0 + in) * NSUB + s;
+            L.trace_in_split = cnt + (CNT_SPLIT0 + in) * NSUB + s;
+            L.trace_out = g->d_lists[1 - in] + o; L.trace_out_n = cnt + (CNT_IN0 + 1 - in) * NSUB + s;
+            L.event = g->d_event + o; L.event_n = cnt + CNT_EVENT * NSUB + s;
+            L.emit = g->d_emit + o; L.emit_n = cnt + CNT_EMIT * NSUB + s;
+            L.grab = g->d_grab + 8 * s; L.next_pkt = g->d_next + s;
+            L.dbg_owner = g->d_owner; L.dbg_iter = cnt + CNT_DBG * NSUB + s;
+            L.P = Ps; L.first = sub_first[s]; L.n = sub_n[s];
+        }
+        return SL;
     };
     const size_t em_lds = G3D ? emit_table_doubles(G.ntheta, G.nphi) * sizeof(double) : 0;
-    auto launch_emit = [&](const Lists& L) {
+    auto launch_emit = [&](const SubLists& L) {
         if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), em_lds, stream, G, R, g->pool, L);
         else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), em_lds, stream, G, R, g->pool, L);
     };
-    const int use = (int)std::min<uint64_t>((uint64_t)P, std::max<uint64_t>(R.n, 1));
+    SubUse use;
+    for (int s = 0; s < NSUB; s++) use.u[s] = (int)std::min<uint64_t>((uint64_t)Ps, std::max<uint64_t>(sub_n[s], 1));
     timed(g, ARTES_K_AUX, stream, [&] {
-        hipLaunchKernelGGL(k_init, dim3((use + 255) / 256), dim3(256), 0, stream, g->pool, g->d_emit, cnt + 3, use);
+        hipLaunchKernelGGL(k_init, dim3(((size_t)P + 255) / 256), dim3(256), 0, stream, g->pool, g->d_emit, cnt + CNT_EMIT * NSUB, Ps, use);
     });
     // pre-iteration: fill the pool; emitted packets go to trace list 0
     {
-        Lists L = lists(1);   // trace_out = list 0
+        SubLists L = lists(1);   // trace_out = list 0
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
-            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + 1, cnt + 0, cnt + 4 + 0, cnt + 2, cnt + 3, g->d_grab, g->d_next,
-                               R.emit_first, P, cnt + 8, R.err);
+            hipLaunchKernelGGL(k_rotate, dim3(NSUB), dim3(64), 0, stream, cnt, 1, g->d_grab, g->d_next, R.emit_first, Ps, R.err);
         });
     }
     HIP_TRY(hipGetLastError());
@@ -437,7 +460,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const char* mi = getenv("ARTES_MAX_IT");
     const long long max_it = mi ? atoll(mi) : 2000000LL;
     for (;;) {
-        Lists L = lists(in);
+        SubLists L = lists(in);
         launch_trace_any<G3D>(g, wpe, trace_bpc, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
             if (pix1 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
@@ -449,8 +472,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         });
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
-            hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, stream, cnt + in, cnt + (1 - in), cnt + 4 + (1 - in), cnt + 2, cnt + 3,
-                               g->d_grab, g->d_next, R.emit_first, P, cnt + 8, R.err);
+            hipLaunchKernelGGL(k_rotate, dim3(NSUB), dim3(64), 0, stream, cnt, in, g->d_grab, g->d_next, R.emit_first, Ps, R.err);
         });
         in = 1 - in;
         it++;
@@ -458,16 +480,18 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
             HIP_TRY(hipGetLastError());
             // (and the watchdog counter: a schedule bug fails the run at once instead of
             // every launch spinning to the watchdog)
-            unsigned long long* h_wd = (unsigned long long*)(g->h_count + 2);
-            HIP_TRY(hipMemcpyAsync(g->h_count, cnt + in, sizeof(int), hipMemcpyDeviceToHost, stream));
+            unsigned long long* h_wd = (unsigned long long*)(g->h_count + NSUB);
+            HIP_TRY(hipMemcpyAsync(g->h_count, cnt + (CNT_IN0 + in) * NSUB, NSUB * sizeof(int), hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipMemcpyAsync(h_wd, R.err + ARTES_ERR_WATCHDOG, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipEventRecord(g->ev_poll, stream));
             HIP_TRY(hipEventSynchronize(g->ev_poll));
             if (*h_wd) return fail(-5, "transport kernel watchdog fired: schedule bug, results invalid");
-            if (*g->h_count == 0) break;
+            long long live = 0;
+            for (int s = 0; s < NSUB; s++) live += g->h_count[s];
+            if (live == 0) break;
         }
         if (it > max_it) {
-            if (getenv("ARTES_VERBOSE")) dump_live(g, cnt + in, g->d_lists[in], cnt + 4 + in, P, stream);
+            if (getenv("ARTES_VERBOSE")) dump_live(g, cnt, in, stream);
             return fail(-5, "event engine did not terminate");
         }
     }
