@@ -591,8 +591,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.batch = bt ? std::max(1, std::min(64, atoi(bt))) : 1;
     const char* bm = getenv("ARTES_BATCH_MIN");
     R.batch_min = bm ? std::max(0, std::min(64, atoi(bm))) : 16;
+    // static share of the trace list in 64ths: 48 on 3D grids, 40 on radial-only ones
+    // (re-swept with the sub-engines: hg 32-40 best, iso flat from 40 to 64)
     const char* sq = getenv("ARTES_STATIC");
-    R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : (grid3d ? 48 : 64);
+    R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : (grid3d ? 48 : 40);
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)
     R.det1 = sin(p->det_theta) * sin(p->det_phi);
     R.det2 = cos(p->det_theta);
