@@ -583,16 +583,15 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
     const char* bw = getenv("ARTES_BACKWARD");
     R.backward = bw ? (atoi(bw) != 0) : 1;
-    // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
-    // 3D grids 48, radial-only grids all of it (tools/static_sweep.sh)
     // lanes that park for the batched forced first interaction (kernel_trace.hpp): run the
     // block once this many wait, or once fewer than batch_min lanes still step
     const char* bt = getenv("ARTES_BATCH");
     R.batch = bt ? std::max(1, std::min(64, atoi(bt))) : 1;
     const char* bm = getenv("ARTES_BATCH_MIN");
     R.batch_min = bm ? std::max(0, std::min(64, atoi(bm))) : 16;
-    // static share of the trace list in 64ths: 48 on 3D grids, 40 on radial-only ones
-    // (re-swept with the sub-engines: hg 32-40 best, iso flat from 40 to 64)
+    // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
+    // 48 on 3D grids, 40 on radial-only ones (re-swept with the sub-engines: hg best at
+    // 32-40, iso flat from 40 to 64; tools/static_sweep.sh)
     const char* sq = getenv("ARTES_STATIC");
     R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : (grid3d ? 48 : 40);
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)
