@@ -138,6 +138,26 @@ def test_shard_invariance(require_gpu):
     np.testing.assert_array_equal(a.counters, b.counters)
 
 
+def test_records_do_not_depend_on_the_split(require_gpu):
+    """The engine splits a call's packet ids over 8 XCD-local sub-engines (block b works on
+    sub-engine b mod 8); a packet's record must not depend on which sub-engine, slot or
+    call carries it: calls of 1, 5 (fewer packets than sub-engines), 13 and 4077 packets
+    reproduce the slices of one 4096-packet call bit for bit."""
+    from artes_amd.engine import Grid
+
+    atm = synthetic.make_config("ray3d", nr=8, ntheta=8, nphi=8)
+    grid = Grid(atm, device=0)
+    det, p = _params(driver.default_config(), atm, grid)
+    whole = grid.trace(p, 0, 4096, 99)
+    parts, first = [], 0
+    for n in (1, 5, 13, 4077):
+        parts.append(grid.trace(p, first, n, 99))
+        first += n
+    grid.close()
+    np.testing.assert_array_equal(np.concatenate(parts), whole)
+    assert (whole[:, 1] > 0).any() and (whole[:, 3] == 1).any()
+
+
 def test_device_variant_matches_host_variant(require_gpu):
     import torch
 
