@@ -373,7 +373,9 @@ __device__ void direction_cosine(const DevRun& R, double alpha, double beta, dou
 }
 
 // linear interpolation of the 16 elements at angle acos(mu) between bin centres
-// (ARTES.f90:1448-1530, 4780-4862); P = [180][16] of the cell's matrix
+// (ARTES.f90:1448-1530, 4780-4862); P = [180][RS] of the cell's matrix (RS = 16, or 17
+// in LDS: see k_event)
+template <int RS = 16>
 __device__ __forceinline__ void interp_matrix(const double* __restrict__ P, double acos_mu, double sc[16]) {
     const double deg = acos_mu * 180.0 / PI;
     const int ideg = (int)deg;
@@ -385,10 +387,10 @@ __device__ __forceinline__ void interp_matrix(const double* __restrict__ P, doub
         for (int i = 0; i < 16; i++) sc[i] = P[i];
     } else if (lo == 180) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) sc[i] = P[179 * 16 + i];
+        for (int i = 0; i < 16; i++) sc[i] = P[179 * RS + i];
     } else {
-        const double* x0 = P + (lo - 1) * 16;
-        const double* x1 = P + (up - 1) * 16;
+        const double* x0 = P + (lo - 1) * RS;
+        const double* x1 = P + (up - 1) * RS;
         const double y0 = (double)lo - 0.5, y1 = (double)up - 0.5;
         const double f = (deg - y0) / (y1 - y0);
 #pragma unroll
@@ -431,11 +433,13 @@ __device__ __forceinline__ int cdf_search4(double s, F cdf) {
     return lo;
 }
 
-// scattering_angle_sampling (ARTES.f90:1534-1661) by searching the cumulative tables
+// scattering_angle_sampling (ARTES.f90:1534-1661) by searching the cumulative tables;
+// C = [181][CS] (CS = 4, or 5 in LDS: see k_event)
+template <int CS = 4>
 __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* __restrict__ C, Rng& rng,
                               const double st[4], double& alpha, double& beta) {
     // azimuth: C_b(i) = i (p11 I + p14 V) + (p12 Q + p13 U) SC2(i) + (p12 U - p13 Q) SS2(i)
-    const double p11 = C[180 * 4 + 0], p12 = C[180 * 4 + 1], p13 = C[180 * 4 + 2], p14 = C[180 * 4 + 3];
+    const double p11 = C[180 * CS + 0], p12 = C[180 * CS + 1], p13 = C[180 * CS + 2], p14 = C[180 * CS + 3];
     const double u = p11 * st[0] + p14 * st[3];
     const double v = p12 * st[1] + p13 * st[2];
     const double w = p12 * st[2] - p13 * st[1];
@@ -453,7 +457,7 @@ __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* _
     // polar: C_t(i) = I A1(i) + (c2b Q + s2b U) A2(i) + (c2b U - s2b Q) A3(i) + V A4(i)
     const double k0 = st[0], k1 = c2b * st[1] + s2b * st[2], k2 = c2b * st[2] - s2b * st[1], k3 = st[3];
     auto ct = [&](int j) {
-        const double* a = C + j * 4;
+        const double* a = C + j * CS;
         return k0 * a[0] + k1 * a[1] + k2 * a[2] + k3 * a[3];
     };
     s = rng.uni() * ct(180);

@@ -421,9 +421,24 @@ __device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S
     return 1;
 }
 
+// Layout of the scattering tables a k_event reads: global memory [180][16] matrices and
+// [181][4] cumulative tables, or the LDS copies padded to odd row strides of 17 and 5
+// doubles.  A matrix row is 128 B, so with stride 16 element e of every row falls in the
+// same pair of LDS banks ((a/4) mod 64 for 8-byte reads): lanes interpolating different
+// angles -- the usual case -- serialised up to 16-way on every element read (measured:
+// LDS bank-conflict cycles ~45 % of k_event's).  Stride 17 (34 dwords) spreads rows over
+// 32 bank pairs; stride 5 does the same for the cumulative-table probes.
+template <bool PAD>
+struct TabLayout {
+    static constexpr int RS = PAD ? 17 : 16;            // matrix row stride
+    static constexpr int MAT = NANG * RS;               // doubles per matrix
+    static constexpr int CS = PAD ? 5 : 4;              // cumulative-table entry stride
+    static constexpr int CUM = (NANG + 1) * CS;         // doubles per cumulative table
+};
+
 // one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended); the peel
 // contribution goes to `D` (see DetAcc)
-template <bool PIX1>
+template <bool PIX1, bool PAD>
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, const Line0& L0,
                                          DetAcc<PIX1>& D, uint32_t& c_scat, uint32_t& c_det) {
     {
@@ -445,7 +460,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         unpack_cell(L0.pcell, cr, ct, cp);
         const int cell = cr + G.nr * (ct + G.ntheta * cp);
         const int mid = G.nmat == 1 ? 0 : G.matid[cell];   // uniform atmosphere: no dependent load
-        const double* __restrict__ P = G.mats + (size_t)mid * MAT_DOUBLES;
+        using TL = TabLayout<PAD>;
+        const double* __restrict__ P = G.mats + (size_t)mid * TL::MAT;
         const double tau_peel = L0.tpeel;
         bool drop = false;
         if ((m & FLAG_EXIT) && tau_peel < 50.0) {
@@ -454,7 +470,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             if (mu >= 1.0) mu = 1.0 - 1.e-10;
             else if (mu <= -1.0) mu = -1.0 + 1.e-10;
             double sc[16];
-            interp_matrix(P, acos(mu), sc);
+            interp_matrix<TL::RS>(P, acos(mu), sc);
             double phi_old = atan2(dy, dx);
             if (phi_old < 0.0) phi_old += TWO_PI;
             if (phi_old > TWO_PI) phi_old -= TWO_PI;
@@ -531,11 +547,11 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         if (R.rec) S.d[slot].nscat += 1;
         Rng rng; rng.s0 = L0.r0; rng.s1 = L0.r1;
         double alpha, beta;
-        sample_angles(G, R, G.cums + (size_t)mid * CUM_DOUBLES, rng, st, alpha, beta);
+        sample_angles<TL::CS>(G, R, G.cums + (size_t)mid * TL::CUM, rng, st, alpha, beta);
         double e0, e1, e2;
         direction_cosine(R, alpha, beta, dx, dy, dz, e0, e1, e2);
         double sc[16];
-        interp_matrix(P, acos(alpha), sc);
+        interp_matrix<TL::RS>(P, acos(alpha), sc);
         if (fabs(alpha) < 1.0) {
             double sn[4];
             polarization_rotation(R, alpha, beta, st, sc, dz, e2, sn, false);
@@ -557,9 +573,9 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
 }
 
 // doubles of LDS holding the scattering tables of k_event: matrices, cumulative
-// sampling tables and the azimuth tables
+// sampling tables (padded, TabLayout<true>) and the azimuth tables
 __host__ __device__ inline size_t event_table_doubles(int nmat) {
-    return (size_t)nmat * (MAT_DOUBLES + CUM_DOUBLES) + 2 * (NANG + 1);
+    return (size_t)nmat * (TabLayout<true>::MAT + TabLayout<true>::CUM) + 2 * (NANG + 1);
 }
 
 // peel-off contribution + scattering (ARTES.f90:4765-4984, 819-846).
@@ -584,13 +600,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
     const size_t plane = (size_t)R.nx * R.ny;
     double* lds_next = s_ev;
     if constexpr (LDS_T) {
+        using TL = TabLayout<true>;
         const int nm = G0.nmat * MAT_DOUBLES, nc = G0.nmat * CUM_DOUBLES;
         double* m = s_ev;
-        double* c = m + nm;
-        double* a = c + nc;
+        double* c = m + G0.nmat * TL::MAT;
+        double* a = c + G0.nmat * TL::CUM;
         double* b = a + (NANG + 1);
-        for (int i = threadIdx.x; i < nm; i += BLOCK) m[i] = G0.mats[i];
-        for (int i = threadIdx.x; i < nc; i += BLOCK) c[i] = G0.cums[i];
+        for (int i = threadIdx.x; i < nm; i += BLOCK) m[(i >> 4) * TL::RS + (i & 15)] = G0.mats[i];   // rows of 16 -> 17
+        for (int i = threadIdx.x; i < nc; i += BLOCK) c[(i >> 2) * TL::CS + (i & 3)] = G0.cums[i];    // entries of 4 -> 5
         for (int i = threadIdx.x; i <= NANG; i += BLOCK) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
         G.mats = m; G.cums = c; G.sc2 = a; G.ss2 = b;
         lds_next = b + (NANG + 1);
@@ -623,7 +640,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
 #ifdef ARTES_DEBUG
         if (i < n) dbg_claim(R, L, slot, S.P, 1, slot >= 0 && to_event_list(cur.mode));
 #endif
-        const int dest = slot >= 0 ? event_one<PIX1>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
+        const int dest = slot >= 0 ? event_one<PIX1, LDS_T>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
         if (i < n) L.trace_out[R.emit_first ? L.P - 1 - i : i] = (dest == 1) ? slot : -1;
