@@ -267,10 +267,24 @@ __device__ __forceinline__ void cell_face(const DevGrid& G, const DevRun& R, dou
 }
 
 // ---------------------------------------------------- scattering physics ---
+// sqrt to ~1 ulp for the scattering geometry: the v_rsq_f64 seed, one Newton step on
+// (sqrt, 1/(2 sqrt)) and one residual correction -- 9 instructions against ~25 for the
+// correctly rounded lowering; +0 for +0, NaN below 0 (as sqrt)
+__device__ __forceinline__ double dsqrt(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-g, h, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    const double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return x > 0.0 ? g : (x == 0.0 ? x : __builtin_nan(""));
+}
+
 // mueller_matrix_filler (ARTES.f90:1934-1960): returns c2p, s2p
 __device__ __forceinline__ void mueller(double psi, double& c2p, double& s2p) {
     c2p = cos_b(2.0 * psi);
-    s2p = sqrt(1.0 - c2p * c2p);
+    s2p = dsqrt(1.0 - c2p * c2p);
     if ((psi > HALF_PI && psi < PI) || (psi > 1.5 * PI && psi < TWO_PI) || (psi > -HALF_PI && psi < 0.0) ||
         (psi > -TWO_PI && psi < -1.5 * PI))
         s2p = -s2p;
@@ -281,7 +295,7 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
                                       const double sc[16], double d2, double dn2, double so[4], bool peeling) {
     if (fabs(alpha) < 1.0 && fabs(dn2) < 1.0) {
         double beta2 = 0.0;
-        const double num = (d2 - dn2 * alpha) / (sqrt(1.0 - alpha * alpha) * sqrt(1.0 - dn2 * dn2));
+        const double num = (d2 - dn2 * alpha) / (dsqrt(1.0 - alpha * alpha) * dsqrt(1.0 - dn2 * dn2));
         if (fabs(num) <= 1.0) beta2 = acos(num);
         else if (num > 1.0 && num < 1.00001) beta2 = 0.0;
         else if (num < -1.0 && num > -1.00001) beta2 = PI;
@@ -289,8 +303,8 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
         double c, s;
         mueller(beta, c, s);
         double r0 = si[0], r1 = c * si[1] + s * si[2], r2 = -s * si[1] + c * si[2], r3 = si[3];
-        const double pr = sqrt(r1 * r1 + r2 * r2 + r3 * r3);
-        double norm = (pr > 0.0) ? sqrt(si[1] * si[1] + si[2] * si[2] + si[3] * si[3]) / pr : 1.0;
+        const double pr = dsqrt(r1 * r1 + r2 * r2 + r3 * r3);
+        double norm = (pr > 0.0) ? dsqrt(si[1] * si[1] + si[2] * si[2] + si[3] * si[3]) / pr : 1.0;
         if (norm < 1.0 || norm > 1.0) { r1 *= norm; r2 *= norm; r3 *= norm; }
         double q[4];
 #pragma unroll
@@ -310,8 +324,8 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
         so[1] = c * q[1] + s * q[2];
         so[2] = -s * q[1] + c * q[2];
         so[3] = q[3];
-        const double po = sqrt(so[1] * so[1] + so[2] * so[2] + so[3] * so[3]);
-        norm = (po > 0.0) ? sqrt(q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) / po : 1.0;
+        const double po = dsqrt(so[1] * so[1] + so[2] * so[2] + so[3] * so[3]);
+        norm = (po > 0.0) ? dsqrt(q[1] * q[1] + q[2] * q[2] + q[3] * q[3]) / po : 1.0;
         if (norm < 1.0 || norm > 1.0) { so[1] *= norm; so[2] *= norm; so[3] *= norm; }
     } else if (alpha >= 1.0 && alpha < 1.0001) {
 #pragma unroll
@@ -340,17 +354,17 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
 // direction_cosine (ARTES.f90:1962-2052)
 __device__ void direction_cosine(const DevRun& R, double alpha, double beta, double d0, double d1, double d2,
                                  double& e0, double& e1, double& e2) {
-    const double cto = d2 / sqrt(d0 * d0 + d1 * d1 + d2 * d2);
-    const double sto = sqrt(1.0 - cto * cto);
+    const double cto = d2 / dsqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    const double sto = dsqrt(1.0 - cto * cto);
     double phi_old = atan2(d1, d0);
     if (phi_old < 0.0) phi_old += TWO_PI;
     double ctn = 0.0, phi_new = 0.0, spn = 0.0;
     const bool upper = (beta >= PI && beta < TWO_PI);
     const bool lower = (beta >= 0.0 && beta < PI);
-    if (upper) ctn = cto * alpha + sto * sqrt(1.0 - alpha * alpha) * cos_b(TWO_PI - beta);
-    else if (lower) ctn = cto * alpha + sto * sqrt(1.0 - alpha * alpha) * cos_b(beta);
+    if (upper) ctn = cto * alpha + sto * dsqrt(1.0 - alpha * alpha) * cos_b(TWO_PI - beta);
+    else if (lower) ctn = cto * alpha + sto * dsqrt(1.0 - alpha * alpha) * cos_b(beta);
     else log_err(R, 18);
-    const double stn = sqrt(1.0 - ctn * ctn);
+    const double stn = dsqrt(1.0 - ctn * ctn);
     double num = (alpha - ctn * cto) / (stn * sto);
     if (num >= 1.0) num = 1.0 - 1.e-10;
     else if (num <= -1.0) num = -1.0 + 1.e-10;
@@ -364,8 +378,8 @@ __device__ void direction_cosine(const DevRun& R, double alpha, double beta, dou
     if (phi_new < 0.0) phi_new += TWO_PI;
     if (phi_new > TWO_PI) phi_new -= TWO_PI;
     const double cpn = cos_b(phi_new);
-    if (phi_new >= 0.0 && phi_new < PI) spn = sqrt(1.0 - cpn * cpn);
-    else if (phi_new >= PI && phi_new <= TWO_PI) spn = -sqrt(1.0 - cpn * cpn);
+    if (phi_new >= 0.0 && phi_new < PI) spn = dsqrt(1.0 - cpn * cpn);
+    else if (phi_new >= PI && phi_new <= TWO_PI) spn = -dsqrt(1.0 - cpn * cpn);
     else log_err(R, 21);
     e0 = stn * cpn;
     e1 = stn * spn;

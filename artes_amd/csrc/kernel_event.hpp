@@ -370,7 +370,7 @@ __device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int s
 // outward unit normal of the (oblate) surface at (x, y, z) (ARTES.f90:1378-1384)
 __device__ __forceinline__ void surface_normal(const DevGrid& G, double x, double y, double z, double& n0, double& n1, double& n2) {
     n0 = x / (G.ox * G.ox); n1 = y / (G.oy * G.oy); n2 = z / (G.oz * G.oz);
-    const double norm = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+    const double norm = dsqrt(n0 * n0 + n1 * n1 + n2 * n2);
     n0 /= norm; n1 /= norm; n2 /= norm;
 }
 
@@ -395,7 +395,7 @@ __device__ __forceinline__ int event_surface_hit(const DevGrid& G, const DevRun&
     double n0, n1, n2;
     surface_normal(G, px, py, pz, n0, n1, n2);
     Rng rng; rng.s0 = S.s[slot].r0; rng.s1 = S.s[slot].r1;
-    const double alpha = sqrt(rng.uni());
+    const double alpha = dsqrt(rng.uni());
     const double beta = TWO_PI * rng.uni();
     double e0, e1, e2;
     direction_cosine(R, alpha, beta, n0, n1, n2, e0, e1, e2);
@@ -478,7 +478,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             bool have_out = false;
             double so[4] = {0, 0, 0, 0};
             if (fabs(dz) < 1.0) {
-                const double num = (R.det2 - dz * mu) / (sqrt(1.0 - mu * mu) * sqrt(1.0 - dz * dz));
+                const double num = (R.det2 - dz * mu) / (dsqrt(1.0 - mu * mu) * dsqrt(1.0 - dz * dz));
                 double phs = 0.0;
                 if (fabs(num) < 1.0) phs = acos(num);
                 else if (num >= 1.0) phs = 1.e-10;
