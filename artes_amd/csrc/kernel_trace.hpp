@@ -79,11 +79,9 @@ __device__ __forceinline__ double fast_sqrt(double x) {
 // theta faces 0..ntheta, so every family reads its faces with the same instructions and
 // no per-lane select of coefficients or flags (the phi family reads radial records, and
 // ignores them); phsc[k] = (sin, cos)(phi_k).
-struct alignas(16) FaceRec {
+struct alignas(32) FaceRec {
     double w, off, s;
     int flags, pad;
-    double unused[2];   // 48-byte records: lanes reading different faces spread over 16
-                        // LDS bank positions ((a/4) mod 64) instead of 8 with 32 bytes
 };
 enum : int { FR_PL = 1, FR_KS_OUT = 2, FR_KS_IN = 4, FR_EDGE = 8, FR_BIG_OUT = 16, FR_BIG_IN = 32 };
 
@@ -99,14 +97,14 @@ __host__ __device__ inline size_t trace_table_bytes(int nr, int ntheta, int nphi
 __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double* lds) {
     TraceTabs T;
     FaceRec* fr = (FaceRec*)lds;
-    for (int i = threadIdx.x; i <= G.nr; i += BLOCK) fr[i] = FaceRec{1.0, G.rf2[i], 0.0, FR_KS_IN | FR_BIG_OUT, 0, {0.0, 0.0}};
+    for (int i = threadIdx.x; i <= G.nr; i += BLOCK) fr[i] = FaceRec{1.0, G.rf2[i], 0.0, FR_KS_IN | FR_BIG_OUT, 0};
     for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) {
         const double th = G.thetaf[i];
         const bool cone = G.tplane[i] == 1;
         const double sg = cone ? (th > HALF_PI ? 1.0 : (th < HALF_PI ? -1.0 : 0.0)) : 0.0;
         const int fl = (cone ? 0 : FR_PL) | ((!cone || !(sg < 0.0)) ? FR_KS_OUT : 0) | ((!cone || !(sg > 0.0)) ? FR_KS_IN : 0) |
                        ((i == 0 || i == G.ntheta) ? FR_EDGE : 0) | FR_BIG_OUT | FR_BIG_IN;
-        fr[G.nr + 1 + i] = FaceRec{-G.tan2[i], 0.0, sg, fl, 0, {0.0, 0.0}};
+        fr[G.nr + 1 + i] = FaceRec{-G.tan2[i], 0.0, sg, fl, 0};
     }
     double2* phsc = (double2*)(fr + (G.nr + 1) + (G.ntheta + 1));
     for (int i = threadIdx.x; i < G.nphi; i += BLOCK) phsc[i] = make_double2(G.phis[i], G.phic[i]);
