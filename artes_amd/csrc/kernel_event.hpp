@@ -165,6 +165,13 @@ constexpr int FLAG_ERR = 1 << 9;
 constexpr int PEEL_KIND_SHIFT = 10;   // 0 = after scattering, 1 = thermal, 2 = surface
 
 __device__ __forceinline__ bool is_peel_trace(int mode) { return mode == S_PEEL || mode == S_PEEL_T || mode == S_PEEL_S; }
+// Emit-list entries carry the ended packet's state in bits 27-28 (0: a fresh slot, its
+// record says what it is; 1-3: S_END_EXIT / S_END_ABS / S_END_DROP), so k_emit counts
+// the ends without a dependent read of the record (slots < 2^26, checked at pool size).
+__device__ __forceinline__ int emit_entry(int slot, int mode) {
+    return slot | ((mode >= S_END_EXIT && mode <= S_END_DROP ? mode - S_END_EXIT + 1 : 0) << 27);
+}
+
 __device__ __forceinline__ bool to_event_list(int end) {
     const int b = end & 0xFF;
     return b == S_PEEL_DONE || b == S_SURF_HIT;
@@ -644,7 +651,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
         if (i < n) L.trace_out[R.emit_first ? L.P - 1 - i : i] = (dest == 1) ? slot : -1;
-        wave_append(dest == 2, slot, L.emit, L.emit_n);
+        wave_append(dest == 2, emit_entry(slot, S_END_DROP), L.emit, L.emit_n);   // (event_one set S_END_DROP)
         slot = slot_n;
         slot_n = slot_nn;
         cur = nxt;
@@ -759,10 +766,12 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
     double f_emit = 0.0, f_exit = 0.0;   // thermal flux_emitted / flux_exit (ARTES.f90:607, 780, 953)
     const int n_pad = (n + 63) & ~63;
     for (int i = sub_block() * BLOCK + threadIdx.x; i < n_pad; i += sub_grid() * BLOCK) {
-        const int slot = i < n ? L.emit[i] : -1;
-        const int m = slot >= 0 ? S.s[slot].mode : S_RETIRED;
+        const int e = i < n ? L.emit[i] : -1;
+        const int slot = e >= 0 ? (e & 0x07FFFFFF) : -1, code = e >= 0 ? (e >> 27) & 3 : 0;
+        const int m = code ? S_END_EXIT - 1 + code : (slot >= 0 ? S.s[slot].mode : S_RETIRED);
 #ifdef ARTES_DEBUG
-        if (i < n) dbg_claim(R, L, slot, S.P, 2, m == S_END_EXIT || m == S_END_ABS || m == S_END_DROP || m == S_FRESH);
+        if (i < n) dbg_claim(R, L, slot, S.P, 2, (m == S_END_EXIT || m == S_END_ABS || m == S_END_DROP || m == S_FRESH) &&
+                                                     (slot < 0 || S.s[slot].mode == m));
 #endif
         if (m == S_END_EXIT || m == S_END_ABS || m == S_END_DROP) {
             if (m == S_END_EXIT) c_exit++;

@@ -764,7 +764,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         }
 #endif
         q_event.push(end && to_event_list(end), slot, L.event, L.event_n);
-        q_emit.push(end && !to_event_list(end), slot, L.emit, L.emit_n);
+        q_emit.push(end && !to_event_list(end), emit_entry(slot, end), L.emit, L.emit_n);
     }
     q_event.flush(L.event, L.event_n);
     q_emit.flush(L.emit, L.emit_n);
