@@ -387,6 +387,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
     unsigned long long dbg_steps = 0, dbg_lanes = 0, dbg_refills = 0, dbg_tsteps = 0, dbg_tlanes = 0;
     unsigned long long dbg_anystop = 0, dbg_anyhit = 0, dbg_nstop = 0, dbg_nmove = 0, dbg_nretry = 0, dbg_nsetup = 0;
+    unsigned long long dbg_firuns = 0, dbg_filanes = 0, dbg_reflanes = 0, dbg_hruns = 0, dbg_hlanes = 0;
 #endif
     // packet state (slot line 0) and trace state
     int slot = -1, mode = 0, pcell = 0, pface = 0, ncross = 0;
@@ -492,6 +493,49 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         }
     };
 
+    // The interaction at the end of a propagation (ARTES.f90:705-720), then the
+    // scattering-loop head (788-813): roulette, albedo weight, minimum weight, and the
+    // peel-off trace's start.  About 85 VALU instructions for the one or two lanes of a
+    // wave-step that reach their interaction point; those lanes park (4) instead and the
+    // wave runs the block for R.hbatch of them together.  Returns the slot's end mode
+    // (absorbed) or 0 (the peel-off trace goes on in this lane).
+    auto interaction = [&]() -> int {
+        const double s = fast_div(ttgt - tacc, kext);
+        px = tx + s * nx; py = ty + s * ny; pz = tz + s * nz;
+#ifdef ARTES_DEBUG_GEOM
+        {   // diagnostic build: is the interaction point in the cell's radial shell?
+            const double S2 = ax2 * px * px + by2 * py * py + cz2 * pz * pz;
+            if (S2 < G.rf2[tcr] * (1 - 1e-9) || S2 > G.rf2[tcr + 1] * (1 + 1e-9)) {
+                if (atomicAdd(&R.err[ARTES_ERR_GEOM], 1ULL) < 6)
+                    printf("[geom] hit outside shell: t %.17g %.17g %.17g n %.17g %.17g %.17g cell %d %d %d face %d %d e %.17g %.17g %.17g sides %x s %.17g tsteps %d mode %d S2/rf2 %.17g %.17g\n",
+                           tx, ty, tz, nx, ny, nz, tcr, tct, tcp, tft, tfi, e0, e1, e2, sides, s, tsteps, mode,
+                           S2 / G.rf2[tcr], S2 / G.rf2[tcr + 1]);
+            }
+        }
+#endif
+        pcell = pack_cell(tcr, tct, tcp);
+        pface = 0;
+        if (kb) {   // a backward trace: count the steps the forward one takes
+            c_cross += (uint32_t)(kb - 2 * ncross);
+            ncross = kb - ncross;
+            kb = 0;
+        }
+        if constexpr (FLOW) flow_segment(R.flow_g, R.flow_t, cell, px, py, pz, nx, ny, nz, s, wI, -1);   // (715, 874)
+        const double xi = rng.uni();   // a killed packet's RNG state is not used again
+        bool kill = !R.photon_scattering || xi < R.fstop;
+        if (alb < 1.0 && alb > 0.0) wI *= alb / R.omfstop;
+        kill = kill || wI <= R.pmin;
+        if (kill) return S_END_ABS;
+        // peel-off trace (ARTES.f90:4722-4761) from the interaction point: same cell (kext,
+        // alb stay), no face
+        c_peel++;
+        mode = S_PEEL;
+        tx = px; ty = py; tz = pz;
+        tft = 0; tfi = 0;
+        set_direction_det();
+        return 0;
+    };
+
     // watchdog: a wave runs ~1e4 iterations per launch at the largest pool; a schedule bug
     // must not leave waves spinning on the device (the run then fails with error 57)
     unsigned int iters = 0;
@@ -500,15 +544,32 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             if ((threadIdx.x & 63) == 0) atomicAdd(&R.err[ARTES_ERR_WATCHDOG], 1ULL);
             break;
         }
+        int end = 0;   // 0: continue, else the slot's new mode
         {
             const unsigned long long pk = __ballot(parked != 0);
             if (pk) {
                 const int stepping = __popcll(__ballot(have && parked == 0));
                 // (stepping == 0: every busy lane is parked, and the idle ones may be too few to
                 // refill -- waiting for more would never end)
-                if (__popcll(pk) >= R.batch || stepping < R.batch_min || stepping == 0 || cur.exhausted) {
-                    if (parked) {
+                const bool force = stepping < R.batch_min || stepping == 0 || cur.exhausted;
+                const unsigned long long pf = __ballot(parked & 1), ph = pk & ~pf;
+                if (pf && (__popcll(pf) >= R.batch || force)) {
+#ifdef ARTES_DEBUG_LANES
+                    dbg_firuns++;
+                    dbg_filanes += __popcll(pf);
+#endif
+                    if (parked & 1) {
                         first_interaction(parked & 2);
+                        parked = 0;
+                    }
+                }
+                if (ph && (__popcll(ph) >= R.hbatch || force)) {
+#ifdef ARTES_DEBUG_LANES
+                    dbg_hruns++;
+                    dbg_hlanes += __popcll(ph);
+#endif
+                    if (parked == 4) {
+                        end = interaction();
                         parked = 0;
                     }
                 }
@@ -529,6 +590,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     const int m = (slot >= 0 && slot < S.P) ? S.s[slot].mode : S_FIRST;
                     dbg_claim(R, L, (my < n && pos >= 0 && pos < L.P) ? slot : -2, S.P, 0, m == S_FIRST || m == S_PROP || is_peel_trace(m));
                 }
+#endif
+#ifdef ARTES_DEBUG_LANES
+                dbg_reflanes += __popcll(__ballot(!have && my >= 0 && slot >= 0));
 #endif
                 if (!have && my >= 0 && slot >= 0) {   // -1: a hole left by a dropped or retired packet
                     const Slot* rec = S.s + slot;
@@ -553,11 +617,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         dbg_lanes += __popcll(__ballot(have));
         if (cur.exhausted) { dbg_tsteps++; dbg_tlanes += __popcll(__ballot(have)); }
 #endif
-        int end = 0;   // 0: continue, else the slot's new mode
 #ifdef ARTES_DEBUG_LANES
         bool dbg_s = false, dbg_h = false, dbg_m = false, dbg_r = false, dbg_u = false;
 #endif
-        if (have && !parked) {
+        if (have && !parked && !end) {
             const double k = kext;
             // ------------------------------------------- evaluate one face family
             const int fam = G3D ? __builtin_ctz(pending) : 0;
@@ -594,23 +657,32 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             if (pending == 0) {
                 // ------------------------------------------------ trace step
                 // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
-                double best;
+                // The nearest distance of the three is the reference's choice whenever it
+                // exceeds 1e-9 m (then all of them do); the two-pass rule runs only when it
+                // does not (a crossing at a corner of two families) or nothing is ahead.
+                // (NaN: no crossing; ties go to the lower family, as the reference's order)
+                double best = e0;
                 int w = 0;
-                {   // (NaN: excluded; ties go to the lower family, as the reference's order)
+                if constexpr (G3D) {
+                    best = min_nonan(min_nonan(e0, e1), e2);
+                    w = e0 == best ? 0 : (e1 == best ? 1 : 2);
+                }
+                if (!(best > 1.e-9 && best < INF)) {   // rare
                     const double t0 = or_nan(e0 > 1.e-9, e0);
                     best = t0;
+                    w = 0;
                     if constexpr (G3D) {
                         const double t1 = or_nan(e1 > 1.e-9, e1), t2 = or_nan(e2 > 1.e-9, e2);
                         best = min_nonan(min_nonan(t0, t1), t2);
                         w = t0 == best ? 0 : (t1 == best ? 1 : 2);
                     }
-                }
-                if (!(best < INF)) {   // rare: nothing beyond 1e-9 m
-                    best = e0 > 1.e-12 ? e0 : INF;
-                    w = 0;
-                    if constexpr (G3D) {
-                        if (e1 > 1.e-12 && e1 < best) { best = e1; w = 1; }
-                        if (e2 > 1.e-12 && e2 < best) { best = e2; w = 2; }
+                    if (!(best < INF)) {   // nothing beyond 1e-9 m
+                        best = e0 > 1.e-12 ? e0 : INF;
+                        w = 0;
+                        if constexpr (G3D) {
+                            if (e1 > 1.e-12 && e1 < best) { best = e1; w = 1; }
+                            if (e2 > 1.e-12 && e2 < best) { best = e2; w = 2; }
+                        }
                     }
                 }
                 // next_cell (ARTES.f90:2671-2798): the crossed family's index moves by one
@@ -668,43 +740,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     load_cell();
                     pending = 1 << w;
                 } else if (prop && !err && hit) {
-                    // interaction in this cell (ARTES.f90:705-720), then the scattering-loop
-                    // head (788-813): roulette, albedo weight, minimum weight
-                    const double s = fast_div(ttgt - tacc, k);
-                    px = tx + s * nx; py = ty + s * ny; pz = tz + s * nz;
-#ifdef ARTES_DEBUG_GEOM
-                    {   // diagnostic build: is the interaction point in the cell's radial shell?
-                        const double S2 = ax2 * px * px + by2 * py * py + cz2 * pz * pz;
-                        if (S2 < G.rf2[tcr] * (1 - 1e-9) || S2 > G.rf2[tcr + 1] * (1 + 1e-9)) {
-                            if (atomicAdd(&R.err[ARTES_ERR_GEOM], 1ULL) < 6)
-                                printf("[geom] hit outside shell: t %.17g %.17g %.17g n %.17g %.17g %.17g cell %d %d %d face %d %d e %.17g %.17g %.17g sides %x s %.17g tsteps %d mode %d S2/rf2 %.17g %.17g\n",
-                                       tx, ty, tz, nx, ny, nz, tcr, tct, tcp, tft, tfi, e0, e1, e2, sides, s, tsteps, mode,
-                                       S2 / G.rf2[tcr], S2 / G.rf2[tcr + 1]);
-                        }
-                    }
-#endif
-                    pcell = pack_cell(tcr, tct, tcp);
-                    pface = 0;
-                    if (kb) {   // a backward trace: count the steps the forward one takes
-                        c_cross += (uint32_t)(kb - 2 * ncross);
-                        ncross = kb - ncross;
-                        kb = 0;
-                    }
-                    if constexpr (FLOW) flow_segment(R.flow_g, R.flow_t, cell, px, py, pz, nx, ny, nz, s, wI, -1);   // (715, 874)
-                    const double xi = rng.uni();   // a killed packet's RNG state is not used again
-                    bool kill = !R.photon_scattering || xi < R.fstop;
-                    if (alb < 1.0 && alb > 0.0) wI *= alb / R.omfstop;
-                    kill = kill || wI <= R.pmin;
-                    if (kill) {
-                        end = S_END_ABS;
-                    } else {                                       // peel-off trace (ARTES.f90:4722-4761)
-                        // from the interaction point: same cell (kext, alb stay), no face
-                        c_peel++;
-                        mode = S_PEEL;
-                        tx = px; ty = py; tz = pz;
-                        tft = 0; tfi = 0;
-                        set_direction_det();
-                    }
+                    // the interaction in this cell waits, parked, until enough lanes of the
+                    // wave need it (the top of the loop)
+                    parked = 4;
                 } else if (prop) {
                     if (err) {
                         log_err(R, 3);
@@ -743,19 +781,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         parked = err ? 3 : 1;
                     }
                 }
-                if (end) {   // write the packet state back once
-                    Slot* rec = S.s + slot;
-                    rec->px = px; rec->py = py; rec->pz = pz;
-                    rec->r0 = rng.s0; rec->r1 = rng.s1;
-                    rec->pcell = pcell; rec->pface = pface;
-                    rec->mode = end; rec->ncross = ncross;
-                    rec->wI = wI;
-                    rec->tpeel = tacc;
-                    rec->ttgt = ttgt;
-                    have = false;
-                }
             }   // pending == 0
         }   // have
+        if (end) {   // write the packet state back once
+            Slot* rec = S.s + slot;
+            rec->px = px; rec->py = py; rec->pz = pz;
+            rec->r0 = rng.s0; rec->r1 = rng.s1;
+            rec->pcell = pcell; rec->pface = pface;
+            rec->mode = end; rec->ncross = ncross;
+            rec->wI = wI;
+            rec->tpeel = tacc;
+            rec->ttgt = ttgt;
+            have = false;
+        }
 #ifdef ARTES_DEBUG_LANES
         {
             const unsigned long long bs = __ballot(dbg_s), bh = __ballot(dbg_h), bm = __ballot(dbg_m);
@@ -782,6 +820,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         atomicAdd(&R.err[2], dbg_nmove);
         atomicAdd(&R.err[4], dbg_nretry);
         atomicAdd(&R.err[5], dbg_nsetup);
+        atomicAdd(&R.err[6], dbg_firuns);
+        atomicAdd(&R.err[7], dbg_filanes);
+        atomicAdd(&R.err[8], dbg_reflanes);
+        atomicAdd(&R.err[9], dbg_hruns);
+        atomicAdd(&R.err[10], dbg_hlanes);
     }
 #endif
     const unsigned long long wv = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);

@@ -28,11 +28,16 @@ for name in ("ray3d",):
         C = r.counter("crossings")
         anystop, anyhit, nstop, nmove = int(r.err[48]), int(r.err[61]), int(r.err[1]), int(r.err[2])
         nretry, nsetup = int(r.err[4]), int(r.err[5])
+        firuns, filanes, reflanes = int(r.err[6]), int(r.err[7]), int(r.err[8])
+        hruns, hlanes = int(r.err[9]), int(r.err[10])
         print(f"{name} {env}: {g.last_kernel_ms():.1f} ms ({n / g.last_kernel_ms() / 1e3:.1f} Mpkt/s) trace {kt['trace'][0]:.1f} ms, "
               f"wave-steps {steps:.3e}, lanes/step {lanes / steps:.1f}, crossings/wave-step {C / steps:.1f}, "
               f"steps/refill {steps / max(refills, 1):.1f}, tail steps {tsteps / steps:.3f} at {tlanes / max(tsteps, 1):.1f} lanes, "
               f"iterations with a trace end {anystop / steps:.3f} (lanes {nstop / max(anystop, 1):.2f}), with an interaction {anyhit / steps:.3f}, "
-              f"moving lanes/iteration {nmove / steps:.1f}, other-face retries {nretry / steps:.2f}, set-up evaluations {nsetup / steps:.2f}",
+              f"moving lanes/iteration {nmove / steps:.1f}, other-face retries {nretry / steps:.2f}, set-up evaluations {nsetup / steps:.2f}, "
+              f"first-interaction block in {firuns / steps:.3f} of iterations ({filanes / max(firuns, 1):.2f} lanes), "
+              f"lanes refilled per refill {reflanes / max(refills, 1):.1f}, "
+              f"interaction block in {hruns / steps:.3f} of iterations ({hlanes / max(hruns, 1):.2f} lanes)",
               flush=True)
         for k, v in old.items():
             if v is None:
