@@ -62,6 +62,20 @@ __device__ __forceinline__ double fast_sqrt(double x) {
     return x > 0.0 ? g : 0.0;
 }
 
+// sqrt(x) to ~1 ulp for x >= 0 (x < 0: any value; callers reject those roots): the seed
+// capped so that x = 0 gives 0 * 1e300 = 0 instead of 0 * inf.  (fmin, not an inline
+// v_min: the compiler must see the transcendental's result being read, for gfx950's
+// trans-use hazard wait.)
+__device__ __forceinline__ double fast_sqrt0(double x) {
+    const double y = fmin(__builtin_amdgcn_rsq(x), 1.e300);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-g, h, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    const double d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+
 // ---------------------------------------------------- face tables (LDS) ---
 // The spheres and the theta cones are one quadric form along the ray,
 //     ax2 x^2 + by2 y^2 + w cz2 z^2 - off = 0,
@@ -284,9 +298,12 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     const double w = G3D ? fc.w : 1.0, sg = G3D ? fc.s : 0.0;
     const int fl = G3D ? fc.flags : (FR_KS_IN | FR_BIG_OUT);
     const bool pl = G3D && (fl & FR_PL);
-    const double qa = fma(w, Az, Axy), qb = 2.0 * fma(w, Bz, Bxy), qc = fma(w, Cz, Cxy) - fc.off;
-    const double disc = qb * qb - 4.0 * qa * qc;
-    const double q = -0.5 * (qb + copysign(fast_sqrt(disc), qb));
+    // quadratic_equation (ARTES.f90:4154-4173) in the half-b form: with qb = 2 hb the
+    // reference's disc = qb^2 - 4 qa qc and q = -(qb + sign(qb) sqrt(disc)) / 2 are exactly
+    // 4 disc4 and -(hb + sign(hb) sqrt(disc4)) (power-of-two scalings round alike)
+    const double qa = fma(w, Az, Axy), hb = fma(w, Bz, Bxy), qc = fma(w, Cz, Cxy) - fc.off;
+    const double disc = fma(hb, hb, -(qa * qc));
+    const double q = -(hb + copysign(fast_sqrt0(disc), hb));
     double num0 = 0.0, den0 = 1.0, num1 = 0.0, den1 = 1.0;
     if constexpr (G3D) {
         const double ga = OBL ? G.a : 1.0, gb = OBL ? G.b : 1.0;
