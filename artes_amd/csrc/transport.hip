@@ -575,10 +575,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     const char* env = getenv("ARTES_DEFER");
     R.defer = env ? atoi(env) : 16;
     const char* rf = getenv("ARTES_REFILL");
-    // refill a wave once this many of its lanes are idle (re-swept after the round-2 step
-    // rewrite: 16 for ray3d and hg, iso flat from 16 to 24)
+    // refill a wave once this many of its lanes are idle (re-swept after the batched
+    // interactions: 16 on 3D grids, 20 on radial-only ones)
     const bool grid3d = (T.ntheta > 1 || T.nphi > 1);
-    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : 16;
+    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? 16 : 20);
     const char* ef = getenv("ARTES_EMIT_FIRST");
     R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
     const char* bw = getenv("ARTES_BACKWARD");
