@@ -129,7 +129,9 @@ __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double
 
 // min of two doubles, one v_min_f64 without the canonicalising v_max the IEEE-mode fmin
 // needs on unknown operands.  A quiet-NaN operand (or_nan below: "no crossing") yields the
-// other operand (IEEE minNum); two NaNs yield a NaN.
+// other operand (IEEE minNum); two NaNs yield a NaN.  Its operands must not be the direct
+// result of a transcendental (v_rcp / v_rsq / v_exp ...): the compiler does not insert the
+// gfx950 trans-use hazard wait before inline assembly.
 __device__ __forceinline__ double min_nonan(double a, double b) {
     double r;
     asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
