@@ -769,8 +769,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     } else if (exit) {                             // left the atmosphere
                         end = S_END_EXIT;
                     } else {                                       // reached the surface (ARTES.f90:755-774)
-                        const double xi = rng.uni();
-                        if (xi > R.surface_albedo) {
+                        // (xi > albedo: absorbed; a black surface absorbs whatever xi is, and
+                        // an ended packet's RNG state is not used again, so no draw then)
+                        bool absorbed = true;
+                        if (R.surface_albedo > 0.0) absorbed = rng.uni() > R.surface_albedo;
+                        if (absorbed) {
                             end = S_END_ABS;
                         } else {
                             // Lambertian reflection: k_event turns the packet at the surface point,
