@@ -198,7 +198,10 @@ struct TraceCursor {
 
 __device__ __forceinline__ TraceCursor make_cursor(int n, int static_q64) {
     const int W = sub_grid() * (BLOCK / 64);            // the waves of this sub-engine
-    const int w = sub_block() * (BLOCK / 64) + (threadIdx.x >> 6);
+    // (the wave index through readfirstlane: the compiler then knows the cursor is
+    // wave-uniform, so k_trace's loop, which ends on it, is a uniform loop -- no exec-mask
+    // bookkeeping at its latch)
+    const int w = __builtin_amdgcn_readfirstlane(sub_block() * (BLOCK / 64) + (int)(threadIdx.x >> 6));
     const int nchunk = (int)((((long long)n * static_q64) >> 6) >> 6);
     TraceCursor c;
     c.chunk = w;
@@ -241,7 +244,7 @@ __device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, 
         const int want = k - got;
         unsigned int base = 0;
         if (lane == 0) base = atomicAdd(&cursors[sh], (unsigned int)want);
-        base = __shfl(base, 0);
+        base = __builtin_amdgcn_readlane(base, 0);   // (uniform: an SGPR)
         const long long start = (long long)lo + base;
         const int avail = (int)max(0LL, min((long long)want, (long long)hi - start));
         if (need && rank >= got && rank < got + avail) mine = (int)start + (rank - got);
