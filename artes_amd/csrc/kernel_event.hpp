@@ -216,6 +216,20 @@ __device__ __forceinline__ TraceCursor make_cursor(int n, int static_q64) {
 }
 
 // hand out up to popc(need) list indices to the lanes with `need`; returns this lane's or -1
+// a wave's cursor kept in LDS, read back as wave-uniform (scalar) values
+__device__ __forceinline__ TraceCursor load_cursor(const TraceCursor* p) {
+    TraceCursor c;
+    c.pos = __builtin_amdgcn_readfirstlane(p->pos);
+    c.end = __builtin_amdgcn_readfirstlane(p->end);
+    c.chunk = __builtin_amdgcn_readfirstlane(p->chunk);
+    c.nchunk = __builtin_amdgcn_readfirstlane(p->nchunk);
+    c.stride = __builtin_amdgcn_readfirstlane(p->stride);
+    c.dyn_lo = __builtin_amdgcn_readfirstlane(p->dyn_lo);
+    c.dyn_n = __builtin_amdgcn_readfirstlane(p->dyn_n);
+    c.exhausted = __builtin_amdgcn_readfirstlane((int)p->exhausted) != 0;
+    return c;
+}
+
 __device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, int home, bool need) {
     const int lane = threadIdx.x & 63;
     const unsigned long long mask = __ballot(need);

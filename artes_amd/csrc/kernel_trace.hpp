@@ -399,7 +399,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     __shared__ int s_q[2][BLOCK];
     const int wbase = threadIdx.x & ~63;
     WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
-    TraceCursor cur = make_cursor(n, R.static_q64);
+    // the wave's trace-list cursor lives in LDS between refills (a wave refills every ~10
+    // iterations; kept in registers it occupied scalar registers that the step's lane masks
+    // then had to be copied around, every iteration); only `exhausted` stays in a register
+    __shared__ TraceCursor s_cur[BLOCK / 64];
+    TraceCursor* const my_cur = &s_cur[threadIdx.x >> 6];
+    bool exhausted;
+    {
+        const TraceCursor c0 = make_cursor(n, R.static_q64);
+        if ((threadIdx.x & 63) == 0) *my_cur = c0;
+        __builtin_amdgcn_wave_barrier();
+        exhausted = c0.exhausted;
+    }
     const int fam_all = !G3D ? 1 : (G.nphi > 1 ? 7 : 3);
     const int nrt = G.nr * G.ntheta;        // linear-index stride of phi
     bool have = false;
@@ -570,7 +581,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 const int stepping = __popcll(__ballot(have && parked == 0));
                 // (stepping == 0: every busy lane is parked, and the idle ones may be too few to
                 // refill -- waiting for more would never end)
-                const bool force = stepping < R.batch_min || stepping == 0 || cur.exhausted;
+                const bool force = stepping < R.batch_min || stepping == 0 || exhausted;
                 const unsigned long long pf = __ballot(parked & 1), ph = pk & ~pf;
                 if (pf && (__popcll(pf) >= R.batch || force)) {
 #ifdef ARTES_DEBUG_LANES
@@ -595,10 +606,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             }
         }
         // ---------------------------------------------------------------- refill
-        if (!cur.exhausted) {
+        if (!exhausted) {
             const unsigned long long idle = __ballot(!have);
             if (__popcll(idle) >= R.refill || idle == __ballot(true)) {
+                TraceCursor cur = load_cursor(my_cur);
                 const int my = wave_take(cur, L.grab, home, !have);
+                if ((threadIdx.x & 63) == 0) *my_cur = cur;
+                __builtin_amdgcn_wave_barrier();
+                exhausted = cur.exhausted;
 #ifdef ARTES_DEBUG_LANES
                 dbg_refills++;
 #endif
@@ -630,11 +645,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }
         }
-        if (!__any(have) && cur.exhausted) break;   // (all lanes idle otherwise: every grab was a hole)
+        if (!__any(have) && exhausted) break;   // (all lanes idle otherwise: every grab was a hole)
 #ifdef ARTES_DEBUG_LANES
         dbg_steps++;
         dbg_lanes += __popcll(__ballot(have));
-        if (cur.exhausted) { dbg_tsteps++; dbg_tlanes += __popcll(__ballot(have)); }
+        if (exhausted) { dbg_tsteps++; dbg_tlanes += __popcll(__ballot(have)); }
 #endif
 #ifdef ARTES_DEBUG_LANES
         bool dbg_s = false, dbg_h = false, dbg_m = false, dbg_r = false, dbg_u = false;
