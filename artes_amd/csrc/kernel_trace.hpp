@@ -66,14 +66,35 @@ __device__ __forceinline__ double fast_sqrt(double x) {
 // capped so that x = 0 gives 0 * 1e300 = 0 instead of 0 * inf.  (fmin, not an inline
 // v_min: the compiler must see the transcendental's result being read, for gfx950's
 // trans-use hazard wait.)
-__device__ __forceinline__ double fast_sqrt0(double x) {
-    const double y = fmin(__builtin_amdgcn_rsq(x), 1.e300);
+__device__ __forceinline__ double fast_sqrt0(double x, double cap = 1.e300) {
+    const double y = fmin(__builtin_amdgcn_rsq(x), cap);
     double g = x * y, h = 0.5 * y;
     const double r = fma(-g, h, 0.5);
     g = fma(g, r, g);
     h = fma(h, r, h);
     const double d = fma(-g, g, x);
     return fma(d, h, g);
+}
+
+// The step's threshold constants in vector registers, loaded once per kernel.  gfx950's
+// VOP3 compares and FMAs take no 64-bit literal, so a constant operand is two scalar moves
+// at every use, and with machine LICM off (Makefile) every step rematerialises them; k_trace
+// has vector registers to spare at 4 waves per SIMD on 3D grids (108 of 128), so there the
+// thresholds live in them.  (The inline move makes them opaque: the compiler cannot fold them back.)
+struct TraceK {
+    double tiny, tol, tol_same, huge, cap, step_min, inf;   // 1e-100 1e-15 1e-3 1e100 1e300 1e-9 inf
+};
+__device__ __forceinline__ double vreg(double c) {
+    double r;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "s"(c));
+    return r;
+}
+template <bool IN_VGPRS>
+__device__ __forceinline__ TraceK trace_consts() {
+    if constexpr (IN_VGPRS)
+        return TraceK{vreg(1.e-100), vreg(1.e-15), vreg(1.e-3), vreg(1.e100), vreg(1.e300), vreg(1.e-9), vreg(__builtin_inf())};
+    else
+        return TraceK{1.e-100, 1.e-15, 1.e-3, 1.e100, 1.e300, 1.e-9, __builtin_inf()};
 }
 
 // ---------------------------------------------------- face tables (LDS) ---
@@ -277,7 +298,8 @@ __device__ __forceinline__ double family_eval(const DevGrid& G, const TraceTabs&
 template <bool G3D, bool OBL>
 __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs& T, int fam, double x, double y, double z,
                                                double n0, double n1, double n2, double Axy, double Az, int ft, int fi,
-                                               int cr, int ct, int cp, int pout, double zp, bool alt, bool& outer) {
+                                               int cr, int ct, int cp, int pout, double zp, bool alt, const TraceK& K,
+                                               bool& outer) {
     const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
     const bool isT = G3D && fam == 1;
     const bool isP = G3D && fam == 2;
@@ -305,7 +327,7 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     // 4 disc4 and -(hb + sign(hb) sqrt(disc4)) (power-of-two scalings round alike)
     const double qa = fma(w, Az, Axy), hb = fma(w, Bz, Bxy), qc = fma(w, Cz, Cxy) - fc.off;
     const double disc = fma(hb, hb, -(qa * qc));
-    const double q = -(hb + copysign(fast_sqrt0(disc), hb));
+    const double q = -(hb + copysign(fast_sqrt0(disc, K.cap), hb));
     double num0 = 0.0, den0 = 1.0, num1 = 0.0, den1 = 1.0;
     if constexpr (G3D) {
         const double ga = OBL ? G.a : 1.0, gb = OBL ? G.b : 1.0;
@@ -321,8 +343,8 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     const bool sameA = onfam & (fi == kA), sameB = onfam & (fi == kB);
     // existence: the divisor, and for the quadratic the discriminant
     const bool d_ok = isP | (disc >= 0.0);
-    bool vA = d_ok & (fabs(dA) > 1.e-100);
-    bool vB = d_ok & (fabs(dB) > 1.e-100);
+    bool vA = d_ok & (fabs(dA) > K.tiny);
+    bool vB = d_ok & (fabs(dB) > K.tiny);
     // cone nappe filter (ARTES.f90:3040-3064); sg = 0 never rejects
     if constexpr (G3D) {
         vA = vA & !(sg * fma(rA, n2, z) > 0.0);
@@ -336,17 +358,17 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     const int fsh = ch ? 0 : 1;
     const double A = pl ? zp : rA;
     const bool big = !isP & sameA & ((fl >> (4 + fsh)) & 1);
-    vA = (vA & !pl & (A > 1.e-15) & (!big | (A > 1.e-3))) | (pl & (ch ? (n2 < -1.e-15) : (n2 > 1.e-15)) & (A > 0.0));
-    vB = vB & !pl & (rB > 1.e-15) & (!big | (rB > 1.e-3));
+    vA = (vA & !pl & (A > K.tol) & (!big | (A > K.tol_same))) | (pl & (ch ? (n2 < -K.tol) : (n2 > K.tol)) & (A > 0.0));
+    vB = vB & !pl & (rB > K.tol) & (!big | (rB > K.tol_same));
     // vetoes (ARTES.f90:2899-2960, 3014-3290, 3318, 3346)
     const bool qkill = (fl & FR_EDGE) | (sameA & ((fl >> (1 + fsh)) & 1));
-    const bool sp0_big = !sameA & (fabs(den0) > 0.0) & !(rA < 1.e100);
+    const bool sp0_big = !sameA & (fabs(den0) > 0.0) & !(rA < K.huge);
     const bool killA = isP ? sameA : qkill;
     const bool killB = isP ? (sameB | sp0_big) : qkill;
     // equal roots of a quadratic give no crossing; the 1e100 cap
     const bool eq = !isP & vA & vB & (A == rB);
-    vA = vA & !killA & !eq & (A < 1.e100);
-    vB = vB & !killB & !eq & (rB < 1.e100);
+    vA = vA & !killA & !eq & (A < K.huge);
+    vB = vB & !killB & !eq & (rB < K.huge);
     outer = isP ? (vB & (!vA | (rB < A))) : ch;
     return min_nonan(or_nan(vA, A), or_nan(vB, rB));   // NaN: no crossing
 }
@@ -402,6 +424,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     // the wave's trace-list cursor lives in LDS between refills (a wave refills every ~10
     // iterations; kept in registers it occupied scalar registers that the step's lane masks
     // then had to be copied around, every iteration); only `exhausted` stays in a register
+    // (3D grids without the flow diagnostics: the radial-only kernel keeps its 5th wave
+    // per SIMD at <= 102 registers, the flow kernel has none to spare)
+    const TraceK K = trace_consts<G3D && !FLOW>();
     __shared__ TraceCursor s_cur[BLOCK / 64];
     TraceCursor* const my_cur = &s_cur[threadIdx.x >> 6];
     bool exhausted;
@@ -672,7 +697,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 dm = family_eval<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, outer);
             } else {
                 const bool alt = (sides >> (4 + fam)) & 1;
-                dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, outer);
+                dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
                 retry = (fam != 2) & !alt & !(dm < INF);
             }
             if constexpr (G3D) {
@@ -701,7 +726,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     best = min_nonan(min_nonan(e0, e1), e2);
                     w = e0 == best ? 0 : (e1 == best ? 1 : 2);
                 }
-                if (!(best > 1.e-9 && best < INF)) {   // rare
+                if (!(best > K.step_min && best < K.inf)) {   // rare
                     const double t0 = or_nan(e0 > 1.e-9, e0);
                     best = t0;
                     w = 0;
