@@ -593,9 +593,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 
     // watchdog: a wave runs ~1e4 iterations per launch at the largest pool; a schedule bug
     // must not leave waves spinning on the device (the run then fails with error 57)
-    unsigned int iters = 0;
+    unsigned int iters_left = 1u << 24;
     for (;;) {
-        if (++iters > (1u << 24)) {
+        if (--iters_left == 0) {
             if ((threadIdx.x & 63) == 0) atomicAdd(&R.err[ARTES_ERR_WATCHDOG], 1ULL);
             break;
         }
@@ -698,7 +698,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             } else {
                 const bool alt = (sides >> (4 + fam)) & 1;
                 dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
-                retry = (fam != 2) & !alt & !(dm < INF);
+                retry = (fam != 2) & !alt & !(dm < K.inf);
             }
             if constexpr (G3D) {
                 e0 = fam == 0 ? dm : e0;
@@ -750,23 +750,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 const bool side = (sides >> w) & 1;
                 const int kf = !G3D ? tcr : (w == 0 ? tcr : (w == 1 ? tct : tcp));
                 int kn = kf + (side ? 1 : -1);
-                if constexpr (G3D) {
-                    if (w == 2) kn = kn < 0 ? G.nphi - 1 : (kn == G.nphi ? 0 : kn);
+                if constexpr (G3D) {   // (branch-free: a divergent branch costs more scalar work)
+                    const int wrapped = kn < 0 ? G.nphi - 1 : (kn == G.nphi ? 0 : kn);
+                    kn = w == 2 ? wrapped : kn;
                 }
                 const int nfi = side ? kn : kf;
-                bool err31 = !(best < INF);
                 // a trace of 2^22 steps is a schedule or geometry bug, not a history (~100
                 // crossings per packet, a few thousand at most): drop the packet with error
                 // ARTES_ERR_RUNAWAY instead of spinning
-                if (++tsteps > (1 << 22)) {
-                    err31 = true;
-                    log_err(R, ARTES_ERR_RUNAWAY);
-                }
+                const bool runaway = ++tsteps > (1 << 22);
+                const bool err31 = !(best < K.inf) | runaway;
                 const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
                 const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
                 bool err = err31 | ((tft == 1) & (tfi == G.cell_depth) & surf);
-                if (err31) log_err(R, 31);
-                else if (err) log_err(R, 34);
+                if (err) {   // (one rarely taken branch for the three error codes)
+                    if (runaway) log_err(R, ARTES_ERR_RUNAWAY);
+                    log_err(R, err31 ? 31 : 34);
+                }
                 c_cross++;
                 ncross++;
                 const double tau_cell = best * k;
