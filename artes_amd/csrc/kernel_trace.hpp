@@ -123,10 +123,11 @@ enum : int { FR_PL = 1, FR_KS_OUT = 2, FR_KS_IN = 4, FR_EDGE = 8, FR_BIG_OUT = 1
 struct TraceTabs {
     const FaceRec* fr;
     const double2* phsc;
+    const double2* tcs;   // (cos, sin)(theta_k), for the set-up bounds
 };
 
 __host__ __device__ inline size_t trace_table_bytes(int nr, int ntheta, int nphi) {
-    return sizeof(FaceRec) * ((size_t)(nr + 1) + (size_t)(ntheta + 1)) + sizeof(double2) * (size_t)nphi;
+    return sizeof(FaceRec) * ((size_t)(nr + 1) + (size_t)(ntheta + 1)) + sizeof(double2) * ((size_t)nphi + ntheta + 1);
 }
 
 __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double* lds) {
@@ -143,8 +144,13 @@ __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double
     }
     double2* phsc = (double2*)(fr + (G.nr + 1) + (G.ntheta + 1));
     for (int i = threadIdx.x; i < G.nphi; i += BLOCK) phsc[i] = make_double2(G.phis[i], G.phic[i]);
+    double2* tcs = phsc + G.nphi;
+    for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) {
+        const double c = G.tcos[i];
+        tcs[i] = make_double2(c, sqrt(fmax(0.0, 1.0 - c * c)));
+    }
     __syncthreads();
-    T.fr = fr; T.phsc = phsc;
+    T.fr = fr; T.phsc = phsc; T.tcs = tcs;
     return T;
 }
 
@@ -472,6 +478,43 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     int tsteps = 0;   // steps of the current trace (runaway guard)
     int parked = 0;   // 1: waiting for the batched forced first interaction (3: after a cell error)
 
+    // Lazy set-up (3D grids, one-face evaluation).  A new trace needs every family's
+    // distance before its first step, one family per iteration, so two of every trace's
+    // iterations used to move nothing.  Instead its three cache entries start as LOWER
+    // BOUNDS of the distance to any face of the family, from the position alone: for the
+    // spheres (r_out^2 - r^2) / (2 r_top) and (r^2 - r_in^2) / (2 r_top) (r +- r_k <= 2 r_top);
+    // for a cone the distance to its two generator lines in the packet's meridional plane,
+    // |rho cos th_k -+ z sin th_k| (the plane: |z|); for a phi half-plane the distance to
+    // its plane, |x sin ph_k - y cos ph_k| -- each shrunk by 1e-9 relative and 1 um
+    // absolute against rounding.  A family stays `pending` (bit f) while its entry is a
+    // bound; a lane evaluates its pending families in order and steps as soon as the
+    // nearest entry is an exact one beyond 1e-9 m: the reference's choice, since every
+    // pending family's candidate lies at least as far as its bound (a candidate the rules
+    // veto is farther still).  Bounds shrink by each step like the distances.  Elsewhere
+    // (oblate grids, the two-face A/B build, the flow kernel, radial-only grids) the entries start at 0, so
+    // every family is evaluated before the first step, as before.
+    constexpr bool LAZY = G3D && !OBL && !TWOFACE && !FLOW;
+    const double inv2rtop = LAZY ? 0.5 / sqrt(G.rf2[G.nr]) : 0.0;
+    auto set_bounds = [&]() {
+        if constexpr (LAZY) {
+            const double r2 = fma(tx, tx, fma(ty, ty, tz * tz));
+            const double br = min_nonan(T.fr[tcr + 1].off - r2, r2 - T.fr[tcr].off) * inv2rtop;
+            const double rho = fast_sqrt(fma(tx, tx, ty * ty));
+            const double2 c0 = T.tcs[tct], c1 = T.tcs[tct + 1];
+            const double bt = min_nonan(min_nonan(fabs(fma(rho, c0.x, -tz * c0.y)), fabs(fma(rho, c0.x, tz * c0.y))),
+                                        min_nonan(fabs(fma(rho, c1.x, -tz * c1.y)), fabs(fma(rho, c1.x, tz * c1.y))));
+            double bp = K.inf;
+            if (G.nphi > 1) {
+                const double2 s0 = T.phsc[tcp], s1 = T.phsc[tcp + 1 == G.nphi ? 0 : tcp + 1];
+                bp = min_nonan(fabs(fma(tx, s0.x, -ty * s0.y)), fabs(fma(tx, s1.x, -ty * s1.y)));
+            }
+            e0 = fma(br, 1.0 - 1.e-9, -1.e-6);
+            e1 = fma(bt, 1.0 - 1.e-9, -1.e-6);
+            e2 = fma(bp, 1.0 - 1.e-9, -1.e-6);
+        } else {
+            e0 = 0.0; e1 = 0.0; e2 = 0.0;
+        }
+    };
     // a new direction with its per-trace constants, and a fresh family cache
     const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
     auto set_direction = [&](double d0, double d1, double d2) {
@@ -482,7 +525,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         tsteps = 0;
         pending = fam_all;
         sides = 0;
-        e0 = INF; e1 = INF; e2 = INF;
+        set_bounds();
         if constexpr (G3D) inz = fast_rcp(nz);
     };
     // every peel-off trace runs along the detector direction: its constants once (3D
@@ -501,7 +544,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             tsteps = 0;
             pending = fam_all;
             sides = 0;
-            e0 = INF; e1 = INF; e2 = INF;
+            set_bounds();
         } else {
             set_direction(R.det0, R.det1, R.det2);
         }
@@ -700,6 +743,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
                 retry = (fam != 2) & !alt & !(dm < K.inf);
             }
+            if constexpr (LAZY) dm = retry ? 0.0 : dm;   // (the other face is still to come: no bound)
             if constexpr (G3D) {
                 e0 = fam == 0 ? dm : e0;
                 e1 = fam == 1 ? dm : e1;
@@ -713,20 +757,22 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
             dbg_r = retry; dbg_u = !retry && pending != 0;
 #endif
-            if (pending == 0) {
-                // ------------------------------------------------ trace step
-                // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
-                // The nearest distance of the three is the reference's choice whenever it
-                // exceeds 1e-9 m (then all of them do); the two-pass rule runs only when it
-                // does not (a crossing at a corner of two families) or nothing is ahead.
-                // (NaN: no crossing; ties go to the lower family, as the reference's order)
-                double best = e0;
-                int w = 0;
-                if constexpr (G3D) {
-                    best = min_nonan(min_nonan(e0, e1), e2);
-                    w = e0 == best ? 0 : (e1 == best ? 1 : 2);
-                }
-                if (!(best > K.step_min && best < K.inf)) {   // rare
+            // ---------------------------------------------------- trace step
+            // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
+            // The nearest distance of the three is the reference's choice whenever it
+            // exceeds 1e-9 m (then all of them do); the two-pass rule runs only when it
+            // does not (a crossing at a corner of two families) or nothing is ahead.
+            // (NaN: no crossing; ties go to the lower family, as the reference's order.)
+            // With pending families (bounds), only an exact nearest entry beyond 1e-9 m steps.
+            double best = e0;
+            int w = 0;
+            if constexpr (G3D) {
+                best = min_nonan(min_nonan(e0, e1), e2);
+                w = e0 == best ? 0 : (e1 == best ? 1 : 2);
+            }
+            const bool fast = best > K.step_min && best < K.inf;
+            if (pending == 0 || (LAZY && fast && !((pending >> w) & 1))) {
+                if (!fast) {   // rare (every family exact here)
                     const double t0 = or_nan(e0 > 1.e-9, e0);
                     best = t0;
                     w = 0;
@@ -797,7 +843,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         tcr = kn;
                     }
                     load_cell();
-                    pending = 1 << w;
+                    pending |= 1 << w;
                 } else if (prop && !err && hit) {
                     // the interaction in this cell waits, parked, until enough lanes of the
                     // wave need it (the top of the loop)
