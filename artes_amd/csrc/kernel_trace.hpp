@@ -755,7 +755,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             }
             if (!retry) pending &= pending - 1;
 #ifdef ARTES_DEBUG_LANES
-            dbg_r = retry; dbg_u = !retry && pending != 0;
+            dbg_r = retry; dbg_u = true;   // (evaluated; lanes that also step are subtracted below)
 #endif
             // ---------------------------------------------------- trace step
             // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
@@ -820,7 +820,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 const bool hit = prop && tacc + tau_cell > ttgt;
                 const bool stop = err || exit || surf || hit;
 #ifdef ARTES_DEBUG_LANES
-                dbg_s = stop; dbg_h = prop && hit && !err; dbg_m = !stop;
+                dbg_s = stop; dbg_h = prop && hit && !err; dbg_m = !stop; dbg_u = false;
 #endif
                 if constexpr (FLOW) {
                     if (prop && !err && !hit) {   // the segment to the face (ARTES.f90:728-743, 889-904)

@@ -34,7 +34,7 @@ for name in ("ray3d",):
               f"wave-steps {steps:.3e}, lanes/step {lanes / steps:.1f}, crossings/wave-step {C / steps:.1f}, "
               f"steps/refill {steps / max(refills, 1):.1f}, tail steps {tsteps / steps:.3f} at {tlanes / max(tsteps, 1):.1f} lanes, "
               f"iterations with a trace end {anystop / steps:.3f} (lanes {nstop / max(anystop, 1):.2f}), with an interaction {anyhit / steps:.3f}, "
-              f"moving lanes/iteration {nmove / steps:.1f}, other-face retries {nretry / steps:.2f}, set-up evaluations {nsetup / steps:.2f}, "
+              f"moving lanes/iteration {nmove / steps:.1f}, other-face retries {nretry / steps:.2f}, evaluations without a step {nsetup / steps:.2f}, "
               f"first-interaction block in {firuns / steps:.3f} of iterations ({filanes / max(firuns, 1):.2f} lanes), "
               f"lanes refilled per refill {reflanes / max(refills, 1):.1f}, "
               f"interaction block in {hruns / steps:.3f} of iterations ({hlanes / max(hruns, 1):.2f} lanes)",
