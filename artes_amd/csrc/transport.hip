@@ -591,8 +591,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.batch_min = bm ? std::max(0, std::min(64, atoi(bm))) : 16;
     // lanes whose propagation reached its interaction point park the same way: the
     // interaction block (roulette, albedo weight, peel-off set-up) runs once this many wait
+    // (6 on 3D grids, where the block also computes the peel-off trace's set-up bounds; 4 on
+    // radial-only ones; profiles/r02/refill_hbatch_sweep*.txt)
     const char* hb = getenv("ARTES_HBATCH");
-    R.hbatch = hb ? std::max(1, std::min(64, atoi(hb))) : 4;
+    R.hbatch = hb ? std::max(1, std::min(64, atoi(hb))) : (grid3d ? 6 : 4);
     // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
     // 48 on 3D grids, 40 on radial-only ones (re-swept with the sub-engines: hg best at
     // 32-40, iso flat from 40 to 64; tools/static_sweep.sh)
