@@ -55,6 +55,11 @@ CASES = {
     "ray_phi2_wrap": (dict(name="ray3d", nr=6, ntheta=4, nphi=2), {}),
     "hg_thick_surface": (dict(name="hg", tau=40.0), {}),
     "ray_absorbing": (dict(name="ray3d", nr=8, ntheta=4, nphi=4, omega=0.6), {}),
+    # fine angular grids: many theta / phi faces within a radial shell, so new traces
+    # often step on one family while the others are still set-up bounds (lazy set-up,
+    # kernel_trace.hpp); the thick one scatters ~8 times per packet (many new traces)
+    "ray_fine_angles": (dict(name="ray3d", nr=24, ntheta=30, nphi=48), {}),
+    "ray_fine_thick": (dict(name="ray3d", nr=12, ntheta=18, nphi=24, tau=6.0), {}),
 }
 
 
