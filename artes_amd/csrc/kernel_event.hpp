@@ -615,8 +615,8 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
 #endif
 //  PIX1:  a one-pixel detector: per-lane register sums, reduced over the wave at the end
 //         (DetAcc); no LDS detector then.
-template <bool LDS_T, bool LDS_D, bool PIX1 = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, SubLists SL) {
+template <bool LDS_T, bool LDS_D, bool PIX1 = false, int EB = BLOCK>
+__global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, SubLists SL) {
     static_assert(!(PIX1 && LDS_D), "a one-pixel detector is reduced in registers");
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_ev[];
@@ -630,9 +630,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
         double* c = m + G0.nmat * TL::MAT;
         double* a = c + G0.nmat * TL::CUM;
         double* b = a + (NANG + 1);
-        for (int i = threadIdx.x; i < nm; i += BLOCK) m[(i >> 4) * TL::RS + (i & 15)] = G0.mats[i];   // rows of 16 -> 17
-        for (int i = threadIdx.x; i < nc; i += BLOCK) c[(i >> 2) * TL::CS + (i & 3)] = G0.cums[i];    // entries of 4 -> 5
-        for (int i = threadIdx.x; i <= NANG; i += BLOCK) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
+        for (int i = threadIdx.x; i < nm; i += EB) m[(i >> 4) * TL::RS + (i & 15)] = G0.mats[i];   // rows of 16 -> 17
+        for (int i = threadIdx.x; i < nc; i += EB) c[(i >> 2) * TL::CS + (i & 3)] = G0.cums[i];    // entries of 4 -> 5
+        for (int i = threadIdx.x; i <= NANG; i += EB) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
         G.mats = m; G.cums = c; G.sc2 = a; G.ss2 = b;
         lds_next = b + (NANG + 1);
     }
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
     double* __restrict__ acc = det;
     if constexpr (LDS_D) {
         acc = lds_next;
-        for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) acc[i] = 0.0;
+        for (size_t i = threadIdx.x; i < 9 * plane; i += EB) acc[i] = 0.0;
     }
     if constexpr (LDS_T || LDS_D) __syncthreads();
     DetAcc<PIX1> D;
@@ -651,8 +651,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
     // Software pipeline: the slot ids come two events ahead and line 0 of the next event's
     // record one event ahead, so the record loads (random lines in the pool) overlap the
     // current event's arithmetic instead of stalling at its start.
-    const int stride = sub_grid() * BLOCK;
-    int i = sub_block() * BLOCK + threadIdx.x;
+    const int stride = sub_grid() * EB;
+    int i = sub_block() * EB + threadIdx.x;
     int slot = i < n ? L.event[i] : -1;
     int slot_n = i + stride < n ? L.event[i + stride] : -1;
     Line0 cur;
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ARTES_EVE
     D.flush_wave();
     if constexpr (LDS_D) {
         __syncthreads();
-        for (size_t i = threadIdx.x; i < 9 * plane; i += BLOCK) {
+        for (size_t i = threadIdx.x; i < 9 * plane; i += EB) {
             const double v = acc[i];
             if (v != 0.0) unsafeAtomicAdd(&det[i], v);
         }

@@ -116,12 +116,12 @@ struct artes_grid {
 // resident blocks per CU of `kernel` at `lds` bytes of dynamic LDS (cached per grid: the
 // event engine launches the same few kernels hundreds of times per call)
 template <class K>
-static int blocks_per_cu(artes_grid* g, K kernel, size_t lds) {
+static int blocks_per_cu(artes_grid* g, K kernel, size_t lds, int block = BLOCK) {
     const std::pair<const void*, size_t> key{(const void*)kernel, lds};
     for (const auto& e : g->occ)
         if (e.first == key) return e.second;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, BLOCK, lds) != hipSuccess) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess) per_cu = 1;
     per_cu = std::max(1, per_cu);
     g->occ.push_back({key, per_cu});
     return per_cu;
@@ -404,10 +404,18 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const bool pix1 = (p1 ? atoi(p1) != 0 : true) && R.nx == 1 && R.ny == 1;
     const char* dl = getenv("ARTES_DET_LDS");
     const bool det_lds = !pix1 && (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
+    // k_event's block with both the tables and the detector in LDS: 768 threads, one block
+    // (12 waves, 3 per SIMD at <= 170 VGPRs) per CU sharing one LDS copy, instead of two
+    // 256-thread blocks (2 waves per SIMD, LDS-bound): k_event -7 % on ray3d / hg / iso
+    // (ARTES_EVENT_BLOCK=256 for the old shape)
+    const char* ebs = getenv("ARTES_EVENT_BLOCK");
+    const int ev_block = ebs && atoi(ebs) == 256 ? 256 : 768;
     int ev_blocks = side_blocks;
     if (det_lds) {
         const size_t b = (ev_lds ? ev_bytes : 0) + det_bytes;
-        int per_cu = ev_lds ? blocks_per_cu(g, k_event<true, true>, b) : blocks_per_cu(g, k_event<false, true>, b);
+        int per_cu = ev_lds ? (ev_block == 768 ? blocks_per_cu(g, k_event<true, true, false, 768>, b, 768)
+                                               : blocks_per_cu(g, k_event<true, true>, b))
+                            : blocks_per_cu(g, k_event<false, true>, b);
         const char* eb = getenv("ARTES_EVENT_BPC");
         if (eb) per_cu = std::max(1, atoi(eb));
         ev_blocks = round_sub(per_cu * g->num_cus);
@@ -465,6 +473,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         timed(g, ARTES_K_EVENT, stream, [&] {
             if (pix1 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
             else if (pix1) hipLaunchKernelGGL((k_event<false, false, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+            else if (ev_lds && det_lds && ev_block == 768) hipLaunchKernelGGL((k_event<true, true, false, 768>), dim3(ev_blocks), dim3(768), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds) hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
             else if (det_lds) hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L);
