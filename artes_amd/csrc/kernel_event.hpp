@@ -330,21 +330,27 @@ __device__ __forceinline__ int peel_pixel(const DevRun& R, double px, double py,
 // count) go to `acc` (the block's LDS detector or its HBM copy), plane 9 (the I-only peel
 // count) and the packet moments 12-15 to `det` (the block's HBM copy).  With a one-pixel
 // detector (spectrum / phase, ARTES.f90:453-465) every peel of the grid would add to the
-// same ten addresses, so PIX1 keeps per-lane partial sums in registers instead and
-// reduces them over the wave once, at the end of the kernel (ARTES.f90:4953-4972 sums).
+// same ten addresses, so PIX1 keeps per-lane partial sums instead -- in the lane's own
+// LDS slot (ten doubles, stride = the block size: conflict-free; registers would take the
+// kernel past 168 VGPRs, i.e. 2 waves per SIMD) -- and reduces them over the wave once, at
+// the end of the kernel (ARTES.f90:4953-4972 sums).
 template <bool PIX1>
 struct DetAcc {
     double* __restrict__ det;
     double* __restrict__ acc;
     size_t plane;
-    double r[10];
-    __device__ __forceinline__ void init(double* d, double* a, size_t pl) {
+    double* __restrict__ lane;   // PIX1: this lane's slot, lane[k * stride]
+    int stride;
+    __device__ __forceinline__ void init(double* d, double* a, size_t pl, double* slots = nullptr, int nthreads = 0) {
         det = d; acc = a; plane = pl;
+        if constexpr (PIX1) {
+            lane = slots + threadIdx.x; stride = nthreads;
 #pragma unroll
-        for (int k = 0; k < 10; k++) r[k] = 0.0;
+            for (int k = 0; k < 10; k++) lane[k * stride] = 0.0;
+        }
     }
     __device__ __forceinline__ void add(int k, int pix, double v) {
-        if constexpr (PIX1) r[k] += v;
+        if constexpr (PIX1) lane[k * stride] += v;
         else if (k == 9) unsafeAtomicAdd(&det[9 * plane + pix], v);   // rare (thermal / surface)
         else unsafeAtomicAdd(&acc[k * plane + pix], v);
     }
@@ -353,12 +359,15 @@ struct DetAcc {
         if constexpr (PIX1) {
 #pragma unroll
             for (int k = 0; k < 10; k++) {
-                const double v = wave_sum_f64(r[k]);
+                const double v = wave_sum_f64(lane[k * stride]);
                 if ((threadIdx.x & 63) == 0 && v != 0.0) unsafeAtomicAdd(&det[k * plane], v);
             }
         }
     }
 };
+
+// LDS bytes of the PIX1 per-lane slots of a k_event block
+__host__ __device__ inline size_t pix1_slot_bytes(int block) { return (size_t)10 * block * sizeof(double); }
 
 // a peel that carries Stokes I only (peel_thermal 4577-4583, peel_surface 4684-4690):
 // moments 0 and 4, and the I-only count plane 9 (the reference counts it for I alone)
@@ -613,11 +622,11 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
 #ifndef ARTES_EVENT_WPE
 #define ARTES_EVENT_WPE 2
 #endif
-//  PIX1:  a one-pixel detector: per-lane register sums, reduced over the wave at the end
-//         (DetAcc); no LDS detector then.
+//  PIX1:  a one-pixel detector: per-lane sums in LDS slots after the tables, reduced over
+//         the wave at the end (DetAcc); no LDS detector then.
 template <bool LDS_T, bool LDS_D, bool PIX1 = false, int EB = BLOCK>
 __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, SubLists SL) {
-    static_assert(!(PIX1 && LDS_D), "a one-pixel detector is reduced in registers");
+    static_assert(!(PIX1 && LDS_D), "a one-pixel detector is reduced per lane");
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_ev[];
     DevGrid G = G0;
@@ -644,7 +653,7 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
     }
     if constexpr (LDS_T || LDS_D) __syncthreads();
     DetAcc<PIX1> D;
-    D.init(det, acc, plane);
+    D.init(det, acc, plane, lds_next, EB);
     const int n = *L.event_n;
     uint32_t c_scat = 0, c_det = 0;
     const int n_pad = (n + 63) & ~63;   // whole waves iterate together (wave-aggregated appends)

@@ -420,6 +420,15 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         if (eb) per_cu = std::max(1, atoi(eb));
         ev_blocks = round_sub(per_cu * g->num_cus);
     }
+    // the one-pixel kernel in 768-thread blocks too: the launch bound holds it to 3 waves per
+    // SIMD (<= 168 VGPRs; 211-219 at 256 threads, i.e. 2 waves)
+    const bool pix1_768 = pix1 && ev_block == 768;
+    const size_t p1_bytes = (ev_lds ? ev_bytes : 0) + pix1_slot_bytes(pix1_768 ? 768 : BLOCK);
+    if (pix1_768) {
+        const int per_cu = ev_lds ? blocks_per_cu(g, k_event<true, false, true, 768>, p1_bytes, 768)
+                                  : blocks_per_cu(g, k_event<false, false, true, 768>, p1_bytes, 768);
+        ev_blocks = round_sub(per_cu * g->num_cus);
+    }
     // the packet ids of the call split into NSUB contiguous ranges, one per sub-engine
     const uint64_t chunk = (R.n + NSUB - 1) / NSUB;
     uint64_t sub_first[NSUB], sub_n[NSUB];
@@ -471,8 +480,10 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         SubLists L = lists(in);
         launch_trace_any<G3D>(g, wpe, trace_bpc, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
-            if (pix1 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
-            else if (pix1) hipLaunchKernelGGL((k_event<false, false, true>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
+            if (pix1_768 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true, 768>), dim3(ev_blocks), dim3(768), p1_bytes, stream, G, R, g->pool, L);
+            else if (pix1_768) hipLaunchKernelGGL((k_event<false, false, true, 768>), dim3(ev_blocks), dim3(768), p1_bytes, stream, G, R, g->pool, L);
+            else if (pix1 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L);
+            else if (pix1) hipLaunchKernelGGL((k_event<false, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L);
             else if (ev_lds && det_lds && ev_block == 768) hipLaunchKernelGGL((k_event<true, true, false, 768>), dim3(ev_blocks), dim3(768), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds) hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
