@@ -413,9 +413,9 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     int ev_blocks = side_blocks;
     if (det_lds) {
         const size_t b = (ev_lds ? ev_bytes : 0) + det_bytes;
-        int per_cu = ev_lds ? (ev_block == 768 ? blocks_per_cu(g, k_event<true, true, false, 768>, b, 768)
-                                               : blocks_per_cu(g, k_event<true, true>, b))
-                            : blocks_per_cu(g, k_event<false, true>, b);
+        int per_cu = ev_block == 768 ? (ev_lds ? blocks_per_cu(g, k_event<true, true, false, 768>, b, 768)
+                                               : blocks_per_cu(g, k_event<false, true, false, 768>, b, 768))
+                                     : (ev_lds ? blocks_per_cu(g, k_event<true, true>, b) : blocks_per_cu(g, k_event<false, true>, b));
         const char* eb = getenv("ARTES_EVENT_BPC");
         if (eb) per_cu = std::max(1, atoi(eb));
         ev_blocks = round_sub(per_cu * g->num_cus);
@@ -487,6 +487,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
             else if (ev_lds && det_lds && ev_block == 768) hipLaunchKernelGGL((k_event<true, true, false, 768>), dim3(ev_blocks), dim3(768), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds) hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
+            else if (det_lds && ev_block == 768) hipLaunchKernelGGL((k_event<false, true, false, 768>), dim3(ev_blocks), dim3(768), det_bytes, stream, G, R, g->pool, L);
             else if (det_lds) hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L);
             else hipLaunchKernelGGL((k_event<false, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
         });
