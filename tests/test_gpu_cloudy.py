@@ -61,8 +61,10 @@ def test_cloudy_trajectories_match_oracle(require_gpu, oracle_mod, cloudy, wl):
     assert (np.abs(ref[:, 6]) > 1e-6 * np.abs(ref[:, 0])).mean() > 0.1
 
 
-def test_cloudy_detector_lds_knob(require_gpu, cloudy):
-    """Detector accumulation in LDS or straight to HBM: same packets, same image."""
+@pytest.mark.parametrize("knob", [("ARTES_DET_LDS", "0"), ("ARTES_EVENT_BLOCK", "256")])
+def test_cloudy_detector_lds_knob(require_gpu, cloudy, knob):
+    """Detector accumulation in LDS or straight to HBM, and the LDS-detector k_event with L2
+    tables (401 matrices) in 768- or 256-thread blocks: same packets, same image."""
     import os
 
     from artes_amd.engine import Grid
@@ -73,25 +75,27 @@ def test_cloudy_detector_lds_knob(require_gpu, cloudy):
     grid = Grid(atm, device=0)
     p = driver.run_params(cfg, det, 1, cell_depth=grid.cell_depth(1))
     a = grid.run(p, 0, 200000, 5)
-    old = os.environ.get("ARTES_DET_LDS")
-    os.environ["ARTES_DET_LDS"] = "0"
+    old = os.environ.get(knob[0])
+    os.environ[knob[0]] = knob[1]
     try:
         b = grid.run(p, 0, 200000, 5)
     finally:
         if old is None:
-            os.environ.pop("ARTES_DET_LDS")
+            os.environ.pop(knob[0])
         else:
-            os.environ["ARTES_DET_LDS"] = old
+            os.environ[knob[0]] = old
     grid.close()
     np.testing.assert_allclose(b.det, a.det, rtol=1e-9, atol=1e-300)
     assert np.array_equal(b.counters, a.counters)
 
 
-@pytest.mark.parametrize("source", ["star", "planet"])
-def test_one_pixel_register_sums_knob(require_gpu, cloudy, source):
-    """A one-pixel detector (spectrum / phase) reduces the peel sums in registers over the
-    wave (k_event PIX1) instead of same-address atomics: same packets, same sums (to the
-    summation order), counts exact; the planet source covers the I-only thermal peels."""
+@pytest.mark.parametrize("source,knob", [("star", ("ARTES_PIX1", "0")), ("planet", ("ARTES_PIX1", "0")),
+                                         ("star", ("ARTES_EVENT_BLOCK", "256"))])
+def test_one_pixel_lane_sums_knob(require_gpu, cloudy, source, knob):
+    """A one-pixel detector (spectrum / phase) keeps per-lane peel sums (LDS slots) reduced
+    over the wave (k_event PIX1) instead of same-address atomics, in 768- or 256-thread
+    blocks: same packets, same sums (to the summation order), counts exact; the planet
+    source covers the I-only thermal peels."""
     import os
 
     from artes_amd.engine import Grid
@@ -107,11 +111,11 @@ def test_one_pixel_register_sums_knob(require_gpu, cloudy, source):
     grid = Grid(atm, device=0)
     p = driver.run_params(cfg, det, 0, det_phi=math.radians(40.0), cell_depth=-1 if source == "planet" else grid.cell_depth(0))
     a = grid.run(p, 0, 300000, 5)
-    os.environ["ARTES_PIX1"] = "0"
+    os.environ[knob[0]] = knob[1]
     try:
         b = grid.run(p, 0, 300000, 5)
     finally:
-        os.environ.pop("ARTES_PIX1")
+        os.environ.pop(knob[0])
     grid.close()
     np.testing.assert_allclose(a.det[:2], b.det[:2], rtol=1e-9, atol=1e-300)
     np.testing.assert_array_equal(a.det[2], b.det[2])

@@ -50,10 +50,11 @@ def test_event_and_persistent_engines_agree(require_gpu):
 @pytest.mark.parametrize("knobs", [dict(ARTES_POOL="5000"), dict(ARTES_REFILL="1", ARTES_STATIC="0"),
                                    dict(ARTES_REFILL="64", ARTES_STATIC="64"), dict(ARTES_EVENT_LDS="0", ARTES_DET_LDS="0"), dict(ARTES_WPE="3"),
                                    dict(ARTES_EMIT_FIRST="0"), dict(ARTES_EMIT_FIRST="1", ARTES_POOL="3000"),
-                                   dict(ARTES_BATCH="4", ARTES_BATCH_MIN="24"), dict(ARTES_BATCH="64", ARTES_BATCH_MIN="0")])
+                                   dict(ARTES_BATCH="4", ARTES_BATCH_MIN="24"), dict(ARTES_BATCH="64", ARTES_BATCH_MIN="0"),
+                                   dict(ARTES_EVENT_BLOCK="256")])
 def test_launch_knobs_do_not_change_results(require_gpu, knobs):
-    """Pool size, refill policy, trace-list split, LDS staging, occupancy and the batching
-    of the forced first interaction only change the schedule: per-packet histories and
+    """Pool size, refill policy, trace-list split, LDS staging, occupancy, the k_event block
+    shape and the batching of the forced first interaction only change the schedule: per-packet histories and
     all counters are identical."""
     atm, grid, p = _setup("hg")
     base = grid.run(p, 0, 300000, 99)
