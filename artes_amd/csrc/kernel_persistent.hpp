@@ -315,7 +315,7 @@ __global__ __launch_bounds__(BLOCK) void transport_kernel(DevGrid G, DevRun R) {
                         mode = M_NEW; endst = E_EXIT;
                     } else if (surf) {
                         if (rng.uni() > R.surface_albedo) { mode = M_NEW; endst = E_ABSORBED; }
-                        else { log_err(R, 62); mode = M_NEW; endst = E_DROPPED; }   // Lambertian: not yet supported
+                        else { mode = M_NEW; endst = E_DROPPED; }   // (unreachable: launch() rejects surface reflection for this engine)
                     } else {
                         tau_acc += tau_cell;
                     }

@@ -554,6 +554,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         tx = px; ty = py; tz = pz;
         unpack_cell(pcell, tcr, tct, tcp);
         unpack_face(pface, tft, tfi);
+#ifdef ARTES_DEBUG
+        if (tcr >= G.nr || tct >= G.ntheta || tcp >= G.nphi) {   // (ARTES_ERR_CELL: the run fails; no out-of-range read)
+            log_err(R, ARTES_ERR_CELL);
+            tcr = min(tcr, G.nr - 1); tct = min(tct, G.ntheta - 1); tcp = min(tcp, G.nphi - 1);
+        }
+#endif
         cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
         load_cell();
         set_direction(d0, d1, d2);
@@ -725,7 +731,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         if (have && !parked && !end) {
             const double k = kext;
             // ------------------------------------------- evaluate one face family
+#ifdef ARTES_NBF
+            // development variant: the pending family with the nearest bound first
+            int fam = 0;
+            if constexpr (G3D) {
+                const double b0 = (pending & 1) ? e0 : INF, b1 = (pending & 2) ? e1 : INF, b2 = (pending & 4) ? e2 : INF;
+                fam = (b0 <= b1 && b0 <= b2) ? 0 : (b1 <= b2 ? 1 : 2);
+                fam = ((pending >> fam) & 1) ? fam : __builtin_ctz(pending);
+            }
+#else
             const int fam = G3D ? __builtin_ctz(pending) : 0;
+#endif
             const int pout = G3D ? ((tcp + 1 == G.nphi) ? 0 : tcp + 1) : 0;
             bool outer;
             // the face the family can cross next; the other one if that has no crossing
@@ -753,7 +769,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 e0 = dm;
                 sides = (outer ? 1 : 0) | ((retry ? 1 : 0) << 4);
             }
-            if (!retry) pending &= pending - 1;
+            // the evaluated family's entry is exact now: clear ITS bit.  (The round-2 "nearest
+            // bound first" variant evaluated a family other than the lowest pending one but kept
+            // `pending &= pending - 1`, which clears the LOWEST bit: that family's bound was then
+            // taken for an exact distance, the lane stepped onto it as onto a face, and next_cell
+            // walked the cell indices out of range -- the illegal access of that round, DESIGN.md
+            // §4; ARTES_DEBUG counts such a clear as ARTES_ERR_PENDING.)
+#ifdef ARTES_DEBUG
+            const int pending_before = pending;
+#endif
+#ifdef ARTES_OLD_CLEAR
+            if (!retry) pending &= pending - 1;   // (development build: the round-2 clear)
+#else
+            if (!retry) pending &= ~(1 << fam);
+#endif
+#ifdef ARTES_DEBUG
+            if (!retry && (pending_before & ~pending) != (1 << fam)) log_err(R, ARTES_ERR_PENDING);
+#endif
 #ifdef ARTES_DEBUG_LANES
             dbg_r = retry; dbg_u = true;   // (evaluated; lanes that also step are subtracted below)
 #endif
@@ -809,6 +841,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
                 const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
                 bool err = err31 | ((tft == 1) & (tfi == G.cell_depth) & surf);
+#ifdef ARTES_DEBUG
+                {   // the new index of the crossed family must name a cell unless the trace leaves
+                    // the grid or reaches the surface (ARTES_ERR_CELL: the packet is dropped before
+                    // its out-of-range kappa read, and the run fails)
+                    const int nk = !G3D ? G.nr : (w == 0 ? G.nr : (w == 1 ? G.ntheta : G.nphi));
+                    if (!err && !exit && !surf && (kn < 0 || kn >= nk)) {
+                        log_err(R, ARTES_ERR_CELL);
+                        err = true;
+                    }
+                }
+#endif
                 if (err) {   // (one rarely taken branch for the three error codes)
                     if (runaway) log_err(R, ARTES_ERR_RUNAWAY);
                     log_err(R, err31 ? 31 : 34);
@@ -923,7 +966,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         atomicAdd(&R.err[40], dbg_tsteps);
         atomicAdd(&R.err[41], dbg_tlanes);
         atomicAdd(&R.err[48], dbg_anystop);
-        atomicAdd(&R.err[61], dbg_anyhit);
+        atomicAdd(&R.err[12], dbg_anyhit);
         atomicAdd(&R.err[1], dbg_nstop);
         atomicAdd(&R.err[2], dbg_nmove);
         atomicAdd(&R.err[4], dbg_nretry);

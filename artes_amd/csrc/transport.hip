@@ -768,6 +768,8 @@ static int32_t run_host(artes_grid* g, const artes_run_params* p, uint64_t first
             for (int i = 0; i < ARTES_NUM_ERR; i++) err[i] += e[i];
         if (e[ARTES_ERR_WATCHDOG]) return fail(-5, "transport kernel watchdog fired: schedule bug, results invalid");
         if (e[ARTES_ERR_LISTS]) return fail(-5, "work-list invariant violated (ARTES_DEBUG check): results invalid");
+        if (e[ARTES_ERR_PENDING] || e[ARTES_ERR_CELL])
+            return fail(-5, "k_trace trace-state invariant violated (ARTES_DEBUG check: pending bit / cell index): results invalid");
     }
     if (records) HIP_TRY(hipMemcpy(records, g->d_rec, n * ARTES_TRACE_FIELDS * sizeof(double), hipMemcpyDeviceToHost));
     return 0;

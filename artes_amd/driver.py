@@ -262,6 +262,33 @@ def write_cell_depth(outdir: str, wavelength_m: float, cell_depth: int) -> None:
             f" {_fmt(wavelength_m * 1e6)} {cell_depth}\n")
 
 
+def radial_optical_depths(atm: dict, wl: int) -> tuple[float, float, float]:
+    """Radial optical depths of the column at theta = phi = cell 0 (``grid_initialize(2)``,
+    ``ARTES.f90:2481-2485``): sum over the radial cells i = 0..nr-1, in that order, of
+    (rfront(i+1) - rfront(i)) x the cell's extinction (scattering + absorption, ``2181``),
+    absorption and scattering opacity.  Returns (total, absorption, scattering)."""
+    rf = np.asarray(atm["radial"], dtype=np.float64)
+    sca = np.asarray(atm["scattering"], dtype=np.float64)[wl, 0, 0, :]   # [nwav][nphi][ntheta][nr]
+    ab = np.asarray(atm["absorption"], dtype=np.float64)[wl, 0, 0, :]
+    tot = t_sca = t_abs = 0.0
+    for i in range(rf.size - 1):
+        dr = float(rf[i + 1] - rf[i])
+        tot += dr * float(sca[i] + ab[i])
+        t_sca += dr * float(sca[i])
+        t_abs += dr * float(ab[i])
+    return tot, t_abs, t_sca
+
+
+def write_optical_depth(outdir: str, wavelength_m: float, atm: dict, wl: int) -> None:
+    """``optical_depth.dat`` (``ARTES.f90:2457-2491``): appended once per wavelength in the
+    ``spectrum`` and ``imaging_broad`` modes -- wavelength [micron], total, absorption and
+    scattering radial optical depth."""
+    tot, t_abs, t_sca = radial_optical_depths(atm, wl)
+    _append(os.path.join(outdir, "optical_depth.dat"),
+            " # Wavelength [micron] - Total optical depth - Absorption optical depth - Scattering optical depth\n\n",
+            " " + " ".join(_fmt(v) for v in (wavelength_m * 1e6, tot, t_abs, t_sca)) + "\n")
+
+
 def write_spectrum_line(outdir: str, wavelength_m: float, det: np.ndarray) -> None:
     """``spectrum.dat`` (``ARTES.f90:3591-3621``)."""
     vals = [wavelength_m * 1e6] + [1e-6 * det[0, k, 0, 0] for k in range(4)]

@@ -29,7 +29,12 @@ class EngineUnavailable(RuntimeError):
 
 
 class EngineError(RuntimeError):
-    pass
+    """A failed engine call; ``err`` holds the error-code counts the call returned, when it
+    returned any (e.g. the ARTES_DEBUG invariant counters that made it fail)."""
+
+    def __init__(self, msg: str, err=None):
+        super().__init__(msg)
+        self.err = err
 
 
 def lib():
@@ -91,9 +96,9 @@ def device_count() -> int:
     return lib().artes_device_count()
 
 
-def _check(rc: int, what: str) -> None:
+def _check(rc: int, what: str, err=None) -> None:
     if rc != 0:
-        raise EngineError(f"{what} failed ({rc}): {lib().artes_last_error().decode(errors='replace')}")
+        raise EngineError(f"{what} failed ({rc}): {lib().artes_last_error().decode(errors='replace')}", err)
 
 
 class RunResult:
@@ -167,7 +172,7 @@ class Grid:
         if not (flow_global or flow_latitudinal):
             _check(lib().artes_run(self.h, C.byref(params), int(first), int(n), int(seed), det.ctypes.data_as(dp),
                                    tot.ctypes.data_as(dp), cnt.ctypes.data_as(up), err.ctypes.data_as(up)),
-                   "artes_run")
+                   "artes_run", err)
             return RunResult(det, tot, cnt, err)
         fg = np.zeros((self.nphi, self.ntheta, self.nr, 3)) if flow_global else None
         ft = np.zeros((self.nphi, self.ntheta, self.nr, 4)) if flow_latitudinal else None

@@ -40,7 +40,7 @@ central vacuum inclusion whose volume fraction f is uniform on ``[0, fmax]``, th
 volume kept equal to the solid sphere's (outer radius ``r / (1 - f)**(1/3)``, core
 ``f**(1/3)`` of that), and the cross sections and matrices are averaged over f with the
 midpoint rule on ``nf`` points.  The coated spheres are solved with Bohren & Huffman's
-BHCOAT recurrences (1983, App. B).  ComputePart's own f quadrature is not known (its
+coated-sphere coefficients in Yang's (2003) bounded recurrences (absorbing mantles included).  ComputePart's own f quadrature is not known (its
 binary is absent), so this path is parity-unpinned too; tests/test_mie.py pins the
 coated-sphere solver by its limits (equal indices, vanishing core, vacuum mantle), the
 optical theorem and energy conservation, and DHS by its ``fmax -> 0`` limit.
@@ -150,16 +150,36 @@ def bhmie(x, m: complex, mu):
     return qext, qsca, g, s1, s2
 
 
+def _logderiv_down(z, nmax: int):
+    """D_n(z) = psi_n'(z) / psi_n(z), n = 0..nmax, for complex z (one per size), by downward
+    recurrence from max(nmax, |z|) + 15 (stable for any z, as in :func:`bhmie`)."""
+    nmx = int(max(nmax, np.abs(z).max())) + 15
+    d = np.zeros((nmax + 1, z.size), dtype=np.complex128)
+    dn = np.zeros(z.size, dtype=np.complex128)
+    for n in range(nmx, 0, -1):
+        dn = n / z - 1.0 / (dn + n / z)
+        if n - 1 <= nmax:
+            d[n - 1] = dn
+    return d
+
+
 def bhcoat(x, y, m1: complex, m2: complex, mu):
     """Coated spheres: core size parameters ``x`` and index ``m1``, outer size parameters
     ``y`` (arrays of equal length) and mantle index ``m2``, at scattering-angle cosines
     ``mu``.  Returns ``qext, qsca, s1, s2`` as :func:`bhmie` (without g).
 
-    Bohren & Huffman's BHCOAT (1983, App. B): the mantle's Riccati-Bessel functions and
-    logarithmic derivatives by upward recurrence, the core's influence through the
-    coefficients A_n, B_n, dropped once it is below 1e-8 (the routine's DEL test); the
-    series is truncated at ``y + 4 y^(1/3) + 2``.  As BHCOAT, meant for weakly absorbing
-    mantles and moderate sizes (the DHS of cloud particles).
+    The coefficients of Bohren & Huffman's coated sphere (1983, sec. 8.1), evaluated with
+    bounded quantities only (Yang 2003, Appl. Opt. 42, 1710): in the mantle the radial
+    function is psi_n(z) + c xi_n(z), z = m2 k r; matching the core's log-derivative D_n(m1 x)
+    at the interface fixes c, and the mantle's log-derivative at its outer surface is
+    H_n = (D_n(z2) + w D3_n(z2)) / (1 + w),  w = -(D_n(z1) - H_t) / (D3_n(z1) - H_t) Q_n,
+    with H_t = (m2/m1) D_n(m1 x) (a_n) or (m1/m2) D_n(m1 x) (b_n), z1 = m2 x, z2 = m2 y,
+    D3 = xi'/xi and Q_n = (psi_n/xi_n)(z1) / (psi_n/xi_n)(z2).  D_n by downward recurrence,
+    psi_n xi_n and D3_n = D_n + i/(psi_n xi_n) upward from closed forms at n = 0, and Q_n as
+    a running product -- none of them grows with the mantle's absorption, so an absorbing
+    mantle around a deep core gives the homogeneous outer sphere (|Q_n| ~ exp(-2 Im(m2)(y - x)))
+    instead of the overflow of BHCOAT's upward chi recurrences.  The series is truncated at
+    ``y + 4 y^(1/3) + 2``.
     """
     x = np.atleast_1d(np.asarray(x, dtype=np.float64))
     y = np.atleast_1d(np.asarray(y, dtype=np.float64))
@@ -167,60 +187,49 @@ def bhcoat(x, y, m1: complex, m2: complex, mu):
     if np.any(x <= 0) or np.any(y < x):
         raise ValueError("need 0 < x <= y")
     m1, m2 = complex(m1), complex(m2)
-    x1, x2, y2 = m1 * x, m2 * x, m2 * y
+    if m1.imag < 0 or m2.imag < 0:
+        raise ValueError("refractive indices n + ik need k >= 0")
     nstop = np.floor(y + 4.0 * np.cbrt(y) + 2.0).astype(np.int64)
-    refrel = m2 / m1
-    coated = np.ones(x.size, dtype=bool)          # BHCOAT's IFLAG = 0
-    delta = 1.0e-8
-    # sizes past their own truncation order keep recurring (their terms are masked out) and
-    # may overflow there: those values never reach an active term
-    with np.errstate(all="ignore"):
-        return _bhcoat_series(x, y, m2, mu, x1, x2, y2, nstop, refrel, coated, delta)
-
-
-def _bhcoat_series(x, y, m2, mu, x1, x2, y2, nstop, refrel, coated, delta):
-    d0x1 = np.cos(x1) / np.sin(x1)
-    d0x2 = np.cos(x2) / np.sin(x2)
-    d0y2 = np.cos(y2) / np.sin(y2)
+    nmax = int(nstop.max())
+    zc, z1, z2 = m1 * x + 0j, m2 * x + 0j, m2 * y + 0j
+    dc, d1, d2 = _logderiv_down(zc, nmax), _logderiv_down(z1, nmax), _logderiv_down(z2, nmax)
+    # n = 0: psi_0 xi_0 = (1 - e^{2iz}) / 2, D3_0 = i, Q_0 = (e^{2i z1} - 1) / (e^{2i z2} - 1) e^{2i (z2 - z1)}
+    e1, e2 = np.exp(2j * z1), np.exp(2j * z2)
+    px1, px2 = 0.5 * (1.0 - e1), 0.5 * (1.0 - e2)
+    d31 = np.full(x.size, 1j)
+    d32 = np.full(x.size, 1j)
+    q = (e1 - 1.0) / (e2 - 1.0) * np.exp(2j * (z2 - z1))
     psi0y, psi1y = np.cos(y), np.sin(y)
     chi0y, chi1y = -np.sin(y), np.cos(y)
     xi1y = psi1y - 1j * chi1y
-    chi0y2, chi1y2 = -np.sin(y2), np.cos(y2)
-    chi0x2, chi1x2 = -np.sin(x2), np.cos(x2)
     qext = np.zeros(x.size)
     qsca = np.zeros(x.size)
     pi0 = np.zeros(mu.size)
     pi1 = np.ones(mu.size)
     s1 = np.zeros((x.size, mu.size), dtype=np.complex128)
     s2 = np.zeros((x.size, mu.size), dtype=np.complex128)
-    for n in range(1, int(nstop.max()) + 1):
+    for n in range(1, nmax + 1):
         act = n <= nstop
         rn = float(n)
+        # step psi xi, D3 and Q from n-1 to n (factors with D_{n-1}, D3_{n-1})
+        f1a, f1b = rn / z1 - d1[n - 1], rn / z1 - d31
+        f2a, f2b = rn / z2 - d2[n - 1], rn / z2 - d32
+        px1, px2 = px1 * f1a * f1b, px2 * f2a * f2b
+        q = q * (f1a / f1b) * (f2b / f2a)
+        d31 = d1[n] + 1j / px1
+        d32 = d2[n] + 1j / px2
+        ht_a, ht_b = (m2 / m1) * dc[n], (m1 / m2) * dc[n]
+        wa = -(d1[n] - ht_a) / (d31 - ht_a) * q
+        wb = -(d1[n] - ht_b) / (d31 - ht_b) * q
+        ha = (d2[n] + wa * d32) / (1.0 + wa)
+        hb = (d2[n] + wb * d32) / (1.0 + wb)
         psiy = (2.0 * rn - 1.0) * psi1y / y - psi0y
         chiy = (2.0 * rn - 1.0) * chi1y / y - chi0y
         xiy = psiy - 1j * chiy
-        d1y2 = 1.0 / (rn / y2 - d0y2) - rn / y2
-        d1x1 = 1.0 / (rn / x1 - d0x1) - rn / x1
-        d1x2 = 1.0 / (rn / x2 - d0x2) - rn / x2
-        chix2 = (2.0 * rn - 1.0) * chi1x2 / x2 - chi0x2
-        chiy2 = (2.0 * rn - 1.0) * chi1y2 / y2 - chi0y2
-        chipx2 = chi1x2 - rn * chix2 / x2
-        chipy2 = chi1y2 - rn * chiy2 / y2
-        ancap = (refrel * d1x1 - d1x2) / (refrel * d1x1 * chix2 - chipx2) / (chix2 * d1x2 - chipx2)
-        bncap = (refrel * d1x2 - d1x1) / (refrel * chipx2 - d1x1 * chix2) / (chix2 * d1x2 - chipx2)
-        brack = np.where(coated, ancap * (chiy2 * d1y2 - chipy2), 0.0)
-        crack = np.where(coated, bncap * (chiy2 * d1y2 - chipy2), 0.0)
-        small = ((np.abs(brack * chipy2) <= delta * np.abs(d1y2)) & (np.abs(brack * chiy2) <= delta)
-                 & (np.abs(crack * chipy2) <= delta * np.abs(d1y2)) & (np.abs(crack * chiy2) <= delta))
-        brack = np.where(small, 0.0, brack)
-        crack = np.where(small, 0.0, crack)
-        coated = coated & ~small
-        dnbar = (d1y2 - brack * chipy2) / (1.0 - brack * chiy2)
-        gnbar = (d1y2 - crack * chipy2) / (1.0 - crack * chiy2)
-        an = ((dnbar / m2 + rn / y) * psiy - psi1y) / ((dnbar / m2 + rn / y) * xiy - xi1y)
-        bn = ((m2 * gnbar + rn / y) * psiy - psi1y) / ((m2 * gnbar + rn / y) * xiy - xi1y)
-        an = np.where(act, an, 0.0)
-        bn = np.where(act, bn, 0.0)
+        ca = ha / m2 + rn / y
+        cb = m2 * hb + rn / y
+        an = np.where(act, (ca * psiy - psi1y) / (ca * xiy - xi1y), 0.0)
+        bn = np.where(act, (cb * psiy - psi1y) / (cb * xiy - xi1y), 0.0)
         qsca += (2.0 * rn + 1.0) * (np.abs(an) ** 2 + np.abs(bn) ** 2)
         qext += (2.0 * rn + 1.0) * (an.real + bn.real)
         fn = (2.0 * rn + 1.0) / (rn * (rn + 1.0))
@@ -229,14 +238,16 @@ def _bhcoat_series(x, y, m2, mu, x1, x2, y2, nstop, refrel, coated, delta):
         s2 += fn * (an[:, None] * tau[None, :] + bn[:, None] * pi1[None, :])
         pi_next = ((2.0 * rn + 1.0) * mu * pi1 - (rn + 1.0) * pi0) / rn
         pi0, pi1 = pi1, pi_next
-        psi0y, psi1y = psi1y, psiy
-        chi0y, chi1y = chi1y, chiy
+        psi0y = np.where(act, psi1y, psi0y)
+        psi1y = np.where(act, psiy, psi1y)
+        chi0y = np.where(act, chi1y, chi0y)
+        chi1y = np.where(act, chiy, chi1y)
         xi1y = psi1y - 1j * chi1y
-        chi0x2, chi1x2 = chi1x2, chix2
-        chi0y2, chi1y2 = chi1y2, chiy2
-        d0x1, d0x2, d0y2 = d1x1, d1x2, d1y2
     qsca *= 2.0 / (y * y)
     qext *= 2.0 / (y * y)
+    if not (np.all(np.isfinite(qext)) and np.all(np.isfinite(qsca)) and np.all(np.isfinite(s1))
+            and np.all(np.isfinite(s2))):
+        raise FloatingPointError("bhcoat: non-finite result")
     return qext, qsca, s1, s2
 
 

@@ -9,7 +9,8 @@ the working directory must contain ``input/<atmosphere>/{artes.in,atmosphere.fit
 each ``-k`` is applied after ``artes.in`` and appended to the copied ``artes.in``.
 Outputs: ``output/<name>/{error.log,plot.dat}``, ``output/<name>/output/{stokes.fits,
 error.fits,photometry.dat,normalization.dat,cell_depth.dat}`` (imaging_mono), plus
-``spectrum.dat`` / ``phase.dat`` for the other modes, ``luminosity.dat`` /
+``spectrum.dat`` / ``phase.dat`` for the other modes (with ``optical_depth.dat`` in
+``spectrum`` and ``imaging_broad``), ``luminosity.dat`` /
 ``cell_luminosity.fits`` for the planet source and ``flow_global.fits`` /
 ``flow_latitudinal.fits`` with ``output:flow_global`` / ``output:flow_latitudinal``.
 
@@ -203,6 +204,8 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
             driver.write_cell_depth(out_dir, wavelengths[wl], source(wl)[0])
     elif mode == "spectrum":                              # ARTES.f90:132-166
         for wl in range(wavelengths.size):
+            if r.rank == 0:   # grid_initialize(2) of the wavelength (ARTES.f90:2457-2491)
+                driver.write_optical_depth(out_dir, wavelengths[wl], atm, wl)
             res = transport_call(wl, det.det_phi)
             err_total += res.err
             if r.rank == 0:
@@ -219,6 +222,8 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
         acc = None
         E = 0.0
         for wl in range(wavelengths.size):
+            if r.rank == 0:
+                driver.write_optical_depth(out_dir, wavelengths[wl], atm, wl)
             res = transport_call(wl, det.det_phi)
             err_total += res.err
             acc = res.det[:3].copy() if acc is None else acc + res.det[:3]

@@ -43,7 +43,13 @@
  *     packet is dropped and also counted as error 31); ARTES_ERR_GEOM (60) counts
  *     interaction points outside their cell's radial shell, checked only by
  *     ARTES_DEBUG_GEOM builds (a diagnostic: the reference's oblate star emission
- *     produces such points by design).
+ *     produces such points by design).  Two more are trace-state invariants checked
+ *     only by ARTES_DEBUG builds, after which the run fails with -5 like 58:
+ *     ARTES_ERR_PENDING (61) counts family evaluations of k_trace that clear a
+ *     `pending` bit other than the evaluated family's (a bound would then be taken
+ *     for an exact face distance), ARTES_ERR_CELL (62) counts cell indices outside
+ *     [0, nr) x [0, ntheta) x [0, nphi) after a move or at a trace start (the packet
+ *     is dropped before the out-of-range table read).
  */
 #ifndef ARTES_AMD_H
 #define ARTES_AMD_H
@@ -62,6 +68,8 @@ extern "C" {
 #define ARTES_ERR_LISTS 58
 #define ARTES_ERR_RUNAWAY 59
 #define ARTES_ERR_GEOM 60
+#define ARTES_ERR_PENDING 61
+#define ARTES_ERR_CELL 62
 
 /* Counter slots (uint64_t counters[ARTES_NUM_COUNTERS]). */
 #define ARTES_CNT_CROSSINGS 0   /* cell_face calls (ARTES.f90:2800), all traces   */

@@ -34,3 +34,43 @@ def test_cloudy_atmosphere(tmp_path, oracle_mod):
         p = driver.run_params(cfg, det, wl, cell_depth=og.cell_depth(wl))
         dd, tot, cnt, err, _ = og.run(p, 0, 5000, 9 + wl)
         assert not np.any(err) and dd[0, 0].sum() > 0
+
+
+def test_optical_depth_dat_cloudy_spectrum(tmp_path):
+    """optical_depth.dat (ARTES.f90:2457-2491) of a `spectrum` run on the cloudy input: one
+    appended line per wavelength, wavelength [micron], then the total, absorption and
+    scattering radial optical depth of the column at theta = phi = cell 0, each the sum of
+    (r_{i+1} - r_i) x the cell opacity -- recomputed here by hand from atmosphere.fits."""
+    from test_cli import OracleTransport
+
+    from artes_amd import runner
+
+    d = tmp_path / "input" / "cloudy"
+    synthetic.make_cloudy(str(d))
+    (d / "artes.in").write_text("photon:source=star\ndetector:type=spectrum\nphoton:fstop=1d-5\n")
+    assert runner.run(["cloudy", "500", "-o", "s", "--seed", "3"], root=str(tmp_path),
+                      transport_factory=OracleTransport) == 0
+    text = (tmp_path / "output/s/output/optical_depth.dat").read_text().splitlines()
+    assert text[0].startswith(" # Wavelength [micron] - Total optical depth - Absorption") and text[1] == ""
+    rows = np.array([[float(v) for v in l.split()] for l in text[2:]])
+    atm = atmosphere.read_atmosphere_fits(str(d / "atmosphere.fits"))
+    h = np.diff(atm["radial"])
+    for wl in range(3):
+        sca, ab = atm["scattering"][wl, 0, 0, :], atm["absorption"][wl, 0, 0, :]
+        want = [atm["wavelength"][wl], (h * (sca + ab)).sum(), (h * ab).sum(), (h * sca).sum()]
+        np.testing.assert_allclose(rows[wl], want, rtol=1e-13)
+    assert rows.shape == (3, 4)
+    np.testing.assert_allclose(rows[:, 1], rows[:, 2] + rows[:, 3], rtol=1e-13)
+    assert np.all(rows[:, 2] > 0) and np.all(np.diff(rows[:, 3]) < 0)   # grey absorption; Rayleigh thinner to the red
+    # the column is theta = phi = cell 0 (clear gas), not a cloudy one
+    cloud = (h * (atm["scattering"][0, 1, 2, :] + atm["absorption"][0, 1, 2, :])).sum()
+    assert cloud > rows[0, 1] + 1.0
+    # imaging_broad writes it too; imaging_mono and phase do not
+    (d / "artes.in").write_text("photon:source=star\ndetector:type=imaging_broad\ndetector:pixel=5\n")
+    assert runner.run(["cloudy", "300", "-o", "b", "--seed", "3"], root=str(tmp_path),
+                      transport_factory=OracleTransport) == 0
+    assert (tmp_path / "output/b/output/optical_depth.dat").read_text() == "\n".join(text) + "\n"
+    (d / "artes.in").write_text("photon:source=star\ndetector:type=imaging_mono\ndetector:pixel=5\n")
+    assert runner.run(["cloudy", "300", "-o", "m", "--seed", "3"], root=str(tmp_path),
+                      transport_factory=OracleTransport) == 0
+    assert not (tmp_path / "output/m/output/optical_depth.dat").exists()

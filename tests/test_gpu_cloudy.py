@@ -159,3 +159,6 @@ def test_cloudy_cli_gpu_matches_oracle_cli(require_gpu, cloudy, mode, out):
     np.testing.assert_allclose(g[:, 1:], o[:, 1:], rtol=1e-3, atol=1e-3 * scale)
     assert np.all(o[:, 1] >= 0) and o[:, 1].max() > 0
     assert (root / f"output/g_{mode}/error.log").read_text() == ""
+    if mode == "spectrum":   # optical_depth.dat (ARTES.f90:2457-2491): the same file from both runs
+        od = (root / f"output/g_{mode}/output/optical_depth.dat").read_text()
+        assert od == (root / f"output/o_{mode}/output/optical_depth.dat").read_text() and len(od.splitlines()) == 5

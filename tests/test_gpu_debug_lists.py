@@ -3,7 +3,9 @@ named by exactly one list per stage, positions inside the pool, list modes consi
 checked on the GPU by the ARTES_DEBUG build (artes_amd/lib/libartes_hip_debug.so, built by
 __graft_entry__.build()) over schedules that stress the hand-off: tiny pools (hundreds of
 iterations), the mirrored trace-list order, purely dynamic grabs, thermal + surface events
-and a one-pixel detector.  A violation counts error 58 (ARTES_ERR_LISTS) and fails the run;
+and a one-pixel detector.  A violation counts error 58 (ARTES_ERR_LISTS) and fails the run, as
+do k_trace's trace-state checks (61: a pending bit other than the evaluated family's cleared;
+62: a cell index outside the grid after a move or at a trace start);
 the debug build must also transport exactly the release build's packets."""
 
 import json
@@ -62,5 +64,8 @@ def test_debug_build_list_invariants(require_gpu, case):
     d = _run(dbg, CASES[case])
     r = _run(rel, CASES[case])
     assert d["err"][58] == 0 and d["err"][57] == 0
+    # k_trace trace-state checks: the evaluated family's pending bit is the one cleared, and
+    # every cell index stays inside the grid (ARTES_ERR_PENDING, ARTES_ERR_CELL)
+    assert d["err"][61] == 0 and d["err"][62] == 0
     assert d["cnt"] == r["cnt"] and d["cnt"][3] == 60000
     assert d["det"] == pytest.approx(r["det"], rel=1e-12)

@@ -132,6 +132,45 @@ def test_coated_sphere_energy_and_optical_theorem(y):
     assert qe[0] == pytest.approx(4.0 / y ** 2 * s1[0, 0].real, rel=1e-10)
 
 
+@pytest.mark.parametrize("m", [2.0 + 1.0j, 3.0 + 3.0j, 1.8 + 0.5j])
+def test_coated_sphere_absorbing_mantle(m):
+    """Strongly absorbing mantles at size parameters up to 100 (BHCOAT's upward chi
+    recurrences overflow there and returned NaN): the equal-index and vanishing-core limits
+    are the homogeneous outer sphere, a vacuum mantle the homogeneous core, and a deep void
+    inside an opaque mantle is invisible; everything finite, extinction >= scattering, and
+    the optical theorem holds."""
+    y = np.array([1.0, 10.0, 25.0, 60.0, 100.0])
+    qe, qs, s1, s2 = mie.bhcoat(0.6 * y, y, m, m, MU)
+    qe0, qs0, _, t1, t2 = mie.bhmie(y, m, MU)
+    np.testing.assert_allclose(qe, qe0, rtol=1e-9)
+    np.testing.assert_allclose(qs, qs0, rtol=1e-9)
+    np.testing.assert_allclose(s1, t1, rtol=0, atol=1e-9 * np.abs(t1).max())
+    np.testing.assert_allclose(s2, t2, rtol=0, atol=1e-9 * np.abs(t2).max())
+    qe, qs, s1, _ = mie.bhcoat(1e-4 * y, y, 1.0, m, MU)                      # vanishing vacuum core
+    np.testing.assert_allclose(qe, qe0, rtol=1e-7)
+    np.testing.assert_allclose(qs, qs0, rtol=1e-7)
+    qe, qs, s1, _ = mie.bhcoat(0.7 * y, y, m, 1.0, MU)                       # vacuum mantle
+    qc, qsc, _, tc, _ = mie.bhmie(0.7 * y, m, MU)
+    np.testing.assert_allclose(qe * y ** 2, qc * (0.7 * y) ** 2, rtol=1e-9)
+    np.testing.assert_allclose(s1, tc, rtol=0, atol=1e-9 * np.abs(tc).max())
+    qe, qs, s1, s2 = mie.bhcoat(0.5 * y, y, 1.0, m, MU)                      # a void in the absorber
+    assert np.all(np.isfinite(s1)) and np.all(np.isfinite(s2))
+    assert np.all(qe >= qs) and np.all(qs > 0)
+    _, _, f1, _ = mie.bhcoat(0.5 * y, y, 1.0, m, [1.0])
+    np.testing.assert_allclose(qe, 4.0 / y ** 2 * f1[:, 0].real, rtol=1e-10)   # optical theorem
+    big = 2.0 * m.imag * 0.5 * y > 60.0                                      # exp(-2 Im(m) (y - x)) < 1e-26
+    np.testing.assert_allclose(qe[big], qe0[big], rtol=1e-10)
+
+
+def test_hollow_spheres_absorbing_index():
+    """The distribution of hollow spheres of a strongly absorbing material (fmax = 0.8): finite
+    opacities and matrices (these were NaN)."""
+    for n_k in (3.0 + 3.0j, 1.8 + 0.5j):
+        ri = (np.array([0.3, 1.0]), np.array([n_k.real] * 2), np.array([n_k.imag] * 2))
+        op, sc = mie.mie_opacity(ri, [0.5], nr=40, fmax=0.8, nf=6)
+        assert np.all(np.isfinite(op)) and np.all(np.isfinite(sc)) and op[2, 0] > 0 and op[3, 0] > 0
+
+
 def test_hollow_sphere_distribution():
     """DHS (fmax > 0, opacityMie.py:15,20): the fmax -> 0 limit is the homogeneous
     distribution; voids change the matrix smoothly; material mass (and so the opacity per

@@ -26,7 +26,7 @@ for name in ("ray3d",):
         steps, lanes, refills = int(r.err[0]), int(r.err[30]), int(r.err[32])
         tsteps, tlanes = int(r.err[40]), int(r.err[41])
         C = r.counter("crossings")
-        anystop, anyhit, nstop, nmove = int(r.err[48]), int(r.err[61]), int(r.err[1]), int(r.err[2])
+        anystop, anyhit, nstop, nmove = int(r.err[48]), int(r.err[12]), int(r.err[1]), int(r.err[2])
         nretry, nsetup = int(r.err[4]), int(r.err[5])
         firuns, filanes, reflanes = int(r.err[6]), int(r.err[7]), int(r.err[8])
         hruns, hlanes = int(r.err[9]), int(r.err[10])
