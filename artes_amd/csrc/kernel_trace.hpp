@@ -320,7 +320,10 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     {
         const double off_in = T.fr[e].off;
         const double qa_in = Axy + Az, hb = Bxy + Bz, qc_in = Cxy + Cz - off_in;
-        const bool in_ok = (hb < 0.0) & (hb * hb - qa_in * qc_in >= 0.0) & !same_in;
+        // (the discriminant exactly as the roots below compute it for this face: written
+        // as a plain hb*hb - qa*qc the compiler contracts it into an FMA of its own choosing,
+        // and a grazing ray could then see the inner sphere here but not there, or back)
+        const bool in_ok = (hb < 0.0) & (fma(hb, hb, -(qa_in * qc_in)) >= 0.0) & !same_in;
         ch = isT ? (fma(n2, Cxy + Cz, -z * hb) < 0.0) : !in_ok;
         ch = ch != alt;
     }

@@ -283,9 +283,19 @@ static bool use_event_engine() {
 }
 
 // allocate the packet pool (transport and diagnostic records) and the work lists of the
-// event engine
-static int32_t ensure_pool(artes_grid* g) {
-    if (g->pool_mem) return 0;
+// event engine, sized for a call of n packets: a call queues at most n slots, so the pool
+// holds min(default, n) slots (rounded to whole waves per sub-engine) and grows when a
+// larger call arrives -- a grid that only ever runs small calls (tests, trajectory
+// records) does not hold the full 8.6 GB
+static void free_pool(artes_grid* g) {
+    void* eptrs[] = {g->pool_mem, g->d_lists[0], g->d_lists[1], g->d_event, g->d_emit, g->d_owner};
+    for (void* p : eptrs)
+        if (p) hipFree(p);
+    g->pool_mem = nullptr; g->d_lists[0] = g->d_lists[1] = nullptr; g->d_event = g->d_emit = nullptr; g->d_owner = nullptr;
+    g->pool = Pool{};
+}
+
+static int32_t ensure_pool(artes_grid* g, uint64_t n) {
     const char* env = getenv("ARTES_POOL");
     // 128 Ki slots per CU (33.6 M on MI355X; 4.3 GB of transport records + 4.3 GB of
     // diagnostic ones): every k_trace launch ends in a tail of a few long traces
@@ -295,7 +305,10 @@ static int32_t ensure_pool(artes_grid* g) {
     // DESIGN.md §3)
     long long P = env ? atoll(env) : (long long)g->num_cus * 131072;
     P = std::max<long long>(1024, std::min<long long>(P, 1LL << 26));
-    P -= P % (64 * NSUB);   // NSUB sub-engines of whole waves of slots
+    P = std::min<long long>(P, std::max<long long>((long long)std::min<uint64_t>(n, 1ULL << 26), 1024));
+    P = (P + 64 * NSUB - 1) / (64 * NSUB) * (64 * NSUB);   // NSUB sub-engines of whole waves of slots
+    if (g->pool_mem && g->pool.P >= P) return 0;
+    free_pool(g);
     HIP_TRY(hipMalloc(&g->pool_mem, (size_t)P * (sizeof(Slot) + sizeof(SlotDiag))));
     g->pool.P = (int)P;
     g->pool.s = (Slot*)g->pool_mem;
@@ -304,14 +317,16 @@ static int32_t ensure_pool(artes_grid* g) {
     HIP_TRY(hipMalloc((void**)&g->d_lists[1], (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_event, (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_emit, (size_t)P * 4));
-    HIP_TRY(hipMalloc((void**)&g->d_counts, CNT_FIELDS * NSUB * sizeof(int)));
-    HIP_TRY(hipMalloc((void**)&g->d_grab, 8 * NSUB * sizeof(unsigned int)));
-    HIP_TRY(hipMalloc((void**)&g->d_next, NSUB * sizeof(unsigned long long)));
-    HIP_TRY(hipHostMalloc((void**)&g->h_count, 64, hipHostMallocDefault));
 #ifdef ARTES_DEBUG
     HIP_TRY(hipMalloc((void**)&g->d_owner, (size_t)P * sizeof(int)));
 #endif
-    HIP_TRY(hipEventCreateWithFlags(&g->ev_poll, hipEventDisableTiming));
+    if (!g->d_counts) {
+        HIP_TRY(hipMalloc((void**)&g->d_counts, CNT_FIELDS * NSUB * sizeof(int)));
+        HIP_TRY(hipMalloc((void**)&g->d_grab, 8 * NSUB * sizeof(unsigned int)));
+        HIP_TRY(hipMalloc((void**)&g->d_next, NSUB * sizeof(unsigned long long)));
+        HIP_TRY(hipHostMalloc((void**)&g->h_count, 64, hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&g->ev_poll, hipEventDisableTiming));
+    }
     return 0;
 }
 
@@ -374,7 +389,7 @@ static void dump_live(artes_grid* g, const int* cnt, int in, hipStream_t stream)
 
 template <bool G3D>
 static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R, bool trace, hipStream_t stream) {
-    int32_t rc = ensure_pool(g);
+    int32_t rc = ensure_pool(g, R.n);
     if (rc) return rc;
     const int P = g->pool.P, Ps = P / NSUB;
     HIP_TRY(hipMemsetAsync(g->d_counts, 0, CNT_FIELDS * NSUB * sizeof(int), stream));

@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Benchmark: photon packets per second on the BASELINE.json headline configuration.
 
-Workload (BASELINE.json configs[2]): Rayleigh-polarised atmosphere (full 16-element
-Mueller matrix), 32 x 16 x 32 (r, theta, phi) cells, one wavelength, star source,
-imaging_mono 25 x 25 detector at theta = phi = 90 deg, radial tau = 1, albedo 1.
+Workload: the metric's "32^3 grid" (BASELINE.json `metric`) with BASELINE configs[2]'s
+physics: Rayleigh-polarised atmosphere (full 16-element Mueller matrix), 32 x 32 x 32
+(r, theta, phi) cells, one wavelength, star source, imaging_mono 25 x 25 detector at
+theta = phi = 90 deg, radial tau = 1, albedo 1.  configs[2]'s own 32 x 16 x 32 grid is
+reported beside it (one untimed step, `configs2_32x16x32`), and the Stokes-I parity step
+runs on that grid (the frozen reference runs are of it).
 One step = one `radiative_transfer` call (ARTES.f90:518-1006) of `--packets` packets
 per GPU (default 1e9 = the config's packet count), followed by the RCCL sum-reduce of
 the detector over ranks.  Weak scaling: every GPU transports `--packets` per step.
@@ -69,9 +72,9 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=20171015)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the untimed parity step (profiling passes)")
-    ap.add_argument("--no-variants", action="store_true", help="skip the untimed 32^3-grid leg (profiling passes)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"))
-    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_sq_summary.json"))
+    ap.add_argument("--no-variants", action="store_true", help="skip the untimed configs[2] (32x16x32) leg (profiling passes)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03", "pmc_summary.json"))
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r03", "pmc_sq_summary.json"))
     args = ap.parse_args()
 
     import numpy as np
@@ -89,8 +92,9 @@ def main() -> int:
     per_gpu = int(args.packets)
 
     cfg = driver.default_config()
-    # the survey's inputs for the frozen reference runs (tests/golden/README.md)
-    atm = synthetic.make_config("ray3d", normalizer="simpson")
+    # the headline grid: the metric's 32^3 cells, configs[2]'s physics (the survey's inputs
+    # for the frozen reference runs, tests/golden/README.md, with 32 theta cells)
+    atm = synthetic.make_config("ray3d", ntheta=32, normalizer="simpson", share_matrix=True)
     rtop = float(atm["radial"][-1])
     det_geom = driver.detector_geometry(cfg, rtop)
     grid = Grid(atm, device=dev)
@@ -216,49 +220,54 @@ def main() -> int:
                 traffic_src = os.path.relpath(path, ROOT)
         if key == "sq" and kt:
             limiter = {"source": os.path.relpath(path, ROOT), **next(iter(kt.values()))}
+            if "valu_busy" in limiter and "salu_busy" in limiter:
+                # issue-side limiter: the VALU and SALU wave-instructions' issue cycles (4 per
+                # wave64 instruction on a SIMD) over the SIMD cycles available to the kernel
+                limiter["issue_frac"] = round(limiter["valu_busy"] + limiter["salu_busy"], 4)
     err_rate = {str(i): {"count": int(e), "per_packet": float(e) / n_step} for i, e in enumerate(err_h) if e}
 
-    # Stokes-I parity against the frozen reference run (tests/golden): one more step of the
-    # same workload, untimed, with the packet-level moments the honest per-pixel errors need
-    parity = None
+    # configs[2]'s own grid, 32 x 16 x 32 (r, theta, phi): one untimed step of the same packet
+    # count on rank 0 at N = 1, and (on rank 0 at any N, the other ranks waiting at the final
+    # barrier) the Stokes-I parity step (the frozen reference runs, tests/golden, are of this
+    # grid): one more step, untimed, with the packet-level moments the honest per-pixel
+    # errors need, against the reference's 1e6-packet image
+    parity, cfg2 = None, None
     ref_dir = os.path.join(ROOT, "tests", "golden", "reference_runs", "t_ray3d_ARTES_det_1e6")
-    if os.path.isdir(ref_dir) and not args.no_parity:
-        check = driver.run_params(cfg, det_geom, 0, cell_depth=grid.cell_depth(0), packet_moments=True)
-        det.zero_(); tot2.zero_()
-        grid.run_device(check, 0, per_gpu, args.seed + 1, det.data_ptr(), tot2.data_ptr(), 0, 0, stream.cuda_stream)
-        torch.cuda.synchronize()
-        raw = det.cpu().numpy()
-        E = driver.package_energy(cfg, float(atm["wavelength"][0]) * 1e-6, rtop, per_gpu, det_geom.det_phi)
-        cmp = stats.compare_to_reference(raw, per_gpu, E, det_geom.pixel_scale, stats.load_reference_run(ref_dir), 10**6)
-        ph = driver.photometry(driver.scale_detector(raw[:3], E))
-        ref_ph = stats.load_reference_run(ref_dir)["photometry"]
-        parity = {"stokes_I_rms_z": round(cmp["rms_z"], 4), "stokes_I_mean_z": round(cmp["mean_z"], 4),
-                  "pixels": cmp["n_pixels"], "I_total": ph[0] * 1e-6, "I_total_reference": float(ref_ph[1]),
-                  "reference": "tests/golden/reference_runs/t_ray3d_ARTES_det_1e6 (1e6 packets)",
-                  "sample": f"{per_gpu} packets on rank 0, untimed, packet moments on"}
-
-    # the metric's "32^3 grid": the same workload on 32 x 32 x 32 (r, theta, phi) cells,
-    # one step of the same packet count, rank 0 at N = 1 (the headline value stays configs[2])
-    grid32 = None
-    if world == 1 and not args.no_variants:
-        atm32 = synthetic.make_config("ray3d", ntheta=32, share_matrix=True)
-        g32 = Grid(atm32, device=dev)
-        d32 = driver.detector_geometry(cfg, float(atm32["radial"][-1]))
-        p32 = driver.run_params(cfg, d32, 0, cell_depth=g32.cell_depth(0), packet_moments=False)
-        det.zero_(); tot2.zero_(); cnt.zero_()
-        g32.run_device(p32, 0, 10**7, args.seed, det.data_ptr(), tot2.data_ptr(), 0, 0, stream.cuda_stream)
-        torch.cuda.synchronize()
-        cnt.zero_()
-        t32 = time.perf_counter()
-        g32.run_device(p32, 0, per_gpu, args.seed, det.data_ptr(), tot2.data_ptr(), cnt.data_ptr(), 0, stream.cuda_stream)
-        torch.cuda.synchronize()
-        dt32 = time.perf_counter() - t32
-        c32 = cnt.cpu().numpy().astype(np.float64) / per_gpu
-        grid32 = {"grid": "32x32x32 (r,theta,phi)", "value": round(per_gpu / dt32 / 1e6, 3), "unit": "Mphotons/s",
-                  "packets": per_gpu, "ms": round(dt32 * 1e3, 3),
-                  "events_per_packet": {"crossings": round(c32[0], 3), "scatters": round(c32[1], 4)},
-                  "sample": "one untimed-region step on rank 0, same workload otherwise"}
-        g32.close()
+    if not ((args.no_variants or world > 1) and args.no_parity):
+        atm2 = synthetic.make_config("ray3d", normalizer="simpson", share_matrix=True)
+        g2 = Grid(atm2, device=dev)
+        d2 = driver.detector_geometry(cfg, float(atm2["radial"][-1]))
+        p2 = driver.run_params(cfg, d2, 0, cell_depth=g2.cell_depth(0), packet_moments=False)
+        if world == 1 and not args.no_variants:
+            det.zero_(); tot2.zero_(); cnt.zero_()
+            g2.run_device(p2, 0, 10**7, args.seed, det.data_ptr(), tot2.data_ptr(), 0, 0, stream.cuda_stream)
+            torch.cuda.synchronize()
+            cnt.zero_()
+            t2 = time.perf_counter()
+            g2.run_device(p2, 0, per_gpu, args.seed, det.data_ptr(), tot2.data_ptr(), cnt.data_ptr(), 0, stream.cuda_stream)
+            torch.cuda.synchronize()
+            dt2 = time.perf_counter() - t2
+            c2 = cnt.cpu().numpy().astype(np.float64) / per_gpu
+            cfg2 = {"grid": "32x16x32 (r,theta,phi), BASELINE configs[2]", "value": round(per_gpu / dt2 / 1e6, 3),
+                    "unit": "Mphotons/s", "packets": per_gpu, "ms": round(dt2 * 1e3, 3),
+                    "events_per_packet": {"crossings": round(c2[0], 3), "scatters": round(c2[1], 4)},
+                    "sample": "one untimed-region step on rank 0, same workload otherwise"}
+        if os.path.isdir(ref_dir) and not args.no_parity:
+            check = driver.run_params(cfg, d2, 0, cell_depth=g2.cell_depth(0), packet_moments=True)
+            det.zero_(); tot2.zero_()
+            g2.run_device(check, 0, per_gpu, args.seed + 1, det.data_ptr(), tot2.data_ptr(), 0, 0, stream.cuda_stream)
+            torch.cuda.synchronize()
+            raw = det.cpu().numpy()
+            r2 = float(atm2["radial"][-1])
+            E = driver.package_energy(cfg, float(atm2["wavelength"][0]) * 1e-6, r2, per_gpu, d2.det_phi)
+            cmp = stats.compare_to_reference(raw, per_gpu, E, d2.pixel_scale, stats.load_reference_run(ref_dir), 10**6)
+            ph = driver.photometry(driver.scale_detector(raw[:3], E))
+            ref_ph = stats.load_reference_run(ref_dir)["photometry"]
+            parity = {"stokes_I_rms_z": round(cmp["rms_z"], 4), "stokes_I_mean_z": round(cmp["mean_z"], 4),
+                      "pixels": cmp["n_pixels"], "I_total": ph[0] * 1e-6, "I_total_reference": float(ref_ph[1]),
+                      "reference": "tests/golden/reference_runs/t_ray3d_ARTES_det_1e6 (1e6 packets, 32x16x32 grid)",
+                      "sample": f"{per_gpu} packets on rank 0 on the configs[2] grid, untimed, packet moments on"}
+        g2.close()
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
@@ -277,8 +286,8 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (uniform Rayleigh atmosphere, generated in-process; no checkpoint/dataset)",
-        "config": {"workload": "BASELINE configs[2]: Rayleigh 16-element Mueller, 32x16x32 (r,theta,phi), 1 wavelength, "
-                               "star source, imaging_mono 25x25, tau=1",
+        "config": {"workload": "metric's 32^3 grid with BASELINE configs[2]'s physics: Rayleigh 16-element Mueller, "
+                               "32x32x32 (r,theta,phi), 1 wavelength, star source, imaging_mono 25x25, tau=1",
                    "packets_per_gpu_per_step": per_gpu,
                    "parallelism": f"packet-sharded x{world}" + (f", one {backend} sum all_reduce per step"
                                                                  if backend else ", single process")},
@@ -298,7 +307,7 @@ def main() -> int:
                      "events_per_packet": {"crossings": round(C, 3), "scatters": round(S, 4), "peels": round(P, 4)}},
         "cpu_baseline": cpu,
         "parity": parity,
-        "grid_32cubed": grid32,
+        "configs2_32x16x32": cfg2,
         # reference error codes (error.log numbers) logged in the timed steps, with their rate
         "errors": err_rate,
     }

@@ -69,3 +69,34 @@ def test_debug_build_list_invariants(require_gpu, case):
     assert d["err"][61] == 0 and d["err"][62] == 0
     assert d["cnt"] == r["cnt"] and d["cnt"][3] == 60000
     assert d["det"] == pytest.approx(r["det"], rel=1e-12)
+
+
+def test_debug_build_catches_round2_fault(require_gpu):
+    """The round-2 illegal access reconstructed in a CHECKED build (libartes_hip_nbf_old_debug:
+    the nearest pending bound evaluated first with the round-2 clear of the lowest pending bit,
+    DESIGN.md §4): the debug checks count the wrong clears (61) and the cell indices that then
+    leave the grid (62), drop those packets before their out-of-range read, and fail the run;
+    the shipping clear passes the same checks (test above)."""
+    lib = os.path.join(ROOT, "artes_amd", "lib", "libartes_hip_nbf_old_debug.so")
+    assert os.path.exists(lib), "build() makes the reconstruction library"
+    script = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+from artes_amd import driver, synthetic
+from artes_amd.engine import EngineError, Grid
+atm = synthetic.make_config("ray3d", share_matrix=True)
+cfg = driver.default_config()
+det = driver.detector_geometry(cfg, atm["radial"][-1])
+g = Grid(atm, 0)
+p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0))
+try:
+    g.run(p, 0, 20000, 777)
+    print(json.dumps(dict(failed=False)))
+except EngineError as e:
+    print(json.dumps(dict(failed=True, e61=int(e.err[61]), e62=int(e.err[62]))))
+""".format(root=ROOT)
+    out = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, ARTES_LIB_PATH=lib), cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["failed"] and r["e61"] > 0 and r["e62"] > 0, r

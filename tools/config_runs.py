@@ -12,7 +12,9 @@ configs[4]: self-luminous gas with P-T dependent molecular opacities, 100 wavele
 Every call is one artes_run of the drop-in's production parameters (packet moments off);
 per call: wall time, packets/s, and the per-kernel HIP-event times.
 
-usage: python tools/config_runs.py <out_dir> [--packets 1e8] [--which 3,4]
+usage: python tools/config_runs.py <out_dir> [--packets 1e8] [--which 3,4] [--phases K] [--lambdas K]
+(--phases / --lambdas K: only K of the 73 angles / 50 wavelengths, evenly spaced -- the
+short runs the rocprofv3 counter passes profile)
 """
 import argparse
 import json
@@ -70,6 +72,8 @@ def main():
     ap.add_argument("--packets", type=float, default=1e8)
     ap.add_argument("--which", default="3,4")
     ap.add_argument("--seed", type=int, default=20171015)
+    ap.add_argument("--phases", type=int, default=0, help="run only this many of the 73 phase angles")
+    ap.add_argument("--lambdas", type=int, default=0, help="run only this many of the 50 wavelengths")
     a = ap.parse_args()
     n = int(a.packets)
     os.makedirs(a.out, exist_ok=True)
@@ -85,14 +89,18 @@ def main():
         cfg = driver.default_config()
         cfg.apply("detector:type", "phase")
         phases = [(f"phi={np.degrees(p):.1f}", 0, p) for p in driver.phase_angles()]
+        if a.phases:
+            phases = [phases[i] for i in np.linspace(0, len(phases) - 1, a.phases).round().astype(int)]
         res["phase"] = calls(grid, cfg, atm, phases, n, a.seed)
-        res["phase_summary"] = summary(res["phase"], "phase curve at wavelengths(1) = 0.45 um, 73 angles")
+        res["phase_summary"] = summary(res["phase"], f"phase curve at wavelengths(1) = 0.45 um, {len(phases)} angles")
         cfg = driver.default_config()
         cfg.apply("detector:type", "spectrum")
         det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
         spec = [(f"lambda={w:.4f}", i, det.det_phi) for i, w in enumerate(wl)]
+        if a.lambdas:
+            spec = [spec[i] for i in np.linspace(0, len(spec) - 1, a.lambdas).round().astype(int)]
         res["spectrum"] = calls(grid, cfg, atm, spec, n, a.seed + 1)
-        res["spectrum_summary"] = summary(res["spectrum"], "spectrum over 50 wavelengths")
+        res["spectrum_summary"] = summary(res["spectrum"], f"spectrum over {len(spec)} wavelengths")
         grid.close()
         json.dump(res, open(os.path.join(a.out, "configs3_cloudy.json"), "w"), indent=1)
         print(json.dumps({k: v for k, v in res.items() if "summary" in k}), flush=True)

@@ -35,6 +35,8 @@ for k, c in tot.items():
     wc = c.get("SQ_WAVE_CYCLES", 0.0) or 1.0
     out["kernels"][k] = {
         "valu_busy": round(4.0 * c["SQ_INSTS_VALU"] / (cycles * SIMDS), 4),
+        # SALU wave-instructions take the issuing wave's turn too (4 cycles per SIMD round)
+        "salu_busy": round(4.0 * c.get("SQ_INSTS_SALU", 0.0) / (cycles * SIMDS), 4),
         "fp64_arith_share_of_valu": round(f64 / c["SQ_INSTS_VALU"], 4),
         "wave_cycles_issuing": round(c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, 4),
         "wave_cycles_waiting_memory": round(c.get("SQ_WAIT_ANY", 0.0) / wc, 4),
