@@ -102,7 +102,7 @@ struct Lists {
     unsigned long long* next_pkt;       // packets handed out so far
     int* dbg_owner;                     // ARTES_DEBUG: [P] last (iteration, stage) tag per slot
     int* dbg_iter;                      // ARTES_DEBUG: iteration counter (k_rotate)
-    int P;                              // list capacity: the slots of this sub-engine
+    int P;                              // trace-list capacity: twice the slots of this sub-engine (L2)
     unsigned long long first, n;        // the packet ids of this sub-engine: [first, first + n)
 };
 
@@ -128,10 +128,15 @@ __device__ __forceinline__ int sub_grid() { return (int)gridDim.x / NSUB; }
 //       ends to exactly one), then the output trace list (k_event at its event index,
 //       k_emit at event_n + its emit index, or mirrored from position P-1 downwards with
 //       emit_first); a slot no list names is free;
-//  (L2) list entries are slot ids in [0, P) or -1 (a hole: a dropped or retired packet);
-//       a trace-list position read is < trace_in_n and maps into [0, P) (the mirrored
-//       half: P-1-(j-split), j < trace_in_n); event_n + emit_n <= P, so the two writers
-//       of the output trace list never overlap;
+//  (L2) list entries are slot ids in [0, S) or -1 (a hole: a dropped or retired packet), S
+//       the sub-engine's slots; a trace-list position read is < trace_in_n and maps into
+//       [0, P) (the mirrored half: P-1-(j-split), j < trace_in_n); event_n + emit_n <= P,
+//       so the two writers of the output trace list never overlap.  The trace lists hold
+//       P = 2 S positions: a packet that k_event drops (a peel-off or scattering error)
+//       leaves a hole at its event position AND takes an emit position for the slot's next
+//       packet, so event_n + emit_n reaches 2 S when every event drops -- with S positions
+//       the emit half ran past the list (round 3: the oblate star source, where the
+//       reference's emission fails for every packet, faulted with a call-sized pool);
 //  (L3) a slot's mode matches its list: a trace kind in the trace list, S_PEEL_DONE /
 //       S_SURF_HIT in the event list, an end state (or S_FRESH at the start) in the emit list.
 // A variant that parks unfinished traces of k_trace's tail must give them list positions
@@ -676,7 +681,12 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         const int dest = slot >= 0 ? event_one<PIX1, LDS_T>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
+#ifdef ARTES_DEBUG
+        if (i < n && i >= L.P) atomicAdd(&R.err[ARTES_ERR_LISTS], 1ULL);   // (L2: no write past the list)
+        if (i < n && i < L.P) L.trace_out[R.emit_first ? L.P - 1 - i : i] = (dest == 1) ? slot : -1;
+#else
         if (i < n) L.trace_out[R.emit_first ? L.P - 1 - i : i] = (dest == 1) ? slot : -1;
+#endif
         wave_append(dest == 2, emit_entry(slot, S_END_DROP), L.emit, L.emit_n);   // (event_one set S_END_DROP)
         slot = slot_n;
         slot_n = slot_nn;
@@ -904,7 +914,12 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
             S.d[slot].nscat = 0;
         }
         }   // emit
+#ifdef ARTES_DEBUG
+        if (i < n && out0 + i >= L.P) atomicAdd(&R.err[ARTES_ERR_LISTS], 1ULL);   // (L2: no write past the list)
+        if (i < n && out0 + i < L.P) L.trace_out[out0 + i] = emit ? slot : -1;
+#else
         if (i < n) L.trace_out[out0 + i] = emit ? slot : -1;
+#endif
     }
     const unsigned long long a = wave_sum_u64(c_exit), b = wave_sum_u64(c_abs), c = wave_sum_u64(c_drop),
                              d = wave_sum_u64(c_pkt);

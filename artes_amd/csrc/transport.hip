@@ -313,8 +313,10 @@ static int32_t ensure_pool(artes_grid* g, uint64_t n) {
     g->pool.P = (int)P;
     g->pool.s = (Slot*)g->pool_mem;
     g->pool.d = (SlotDiag*)((char*)g->pool_mem + (size_t)P * sizeof(Slot));
-    HIP_TRY(hipMalloc((void**)&g->d_lists[0], (size_t)P * 4));
-    HIP_TRY(hipMalloc((void**)&g->d_lists[1], (size_t)P * 4));
+    // trace lists hold up to twice the slots: a packet dropped in k_event keeps its event
+    // position (a hole) and takes an emit position as well (kernel_event.hpp, Lists (L2))
+    HIP_TRY(hipMalloc((void**)&g->d_lists[0], (size_t)2 * P * 4));
+    HIP_TRY(hipMalloc((void**)&g->d_lists[1], (size_t)2 * P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_event, (size_t)P * 4));
     HIP_TRY(hipMalloc((void**)&g->d_emit, (size_t)P * 4));
 #ifdef ARTES_DEBUG
@@ -333,15 +335,24 @@ static int32_t ensure_pool(artes_grid* g, uint64_t n) {
 // grids are whole multiples of the sub-engine count (block b works on sub-engine b % NSUB)
 static int round_sub(int blocks) { return std::max(NSUB, (blocks + NSUB - 1) / NSUB * NSUB); }
 
-// k_trace (kernel_trace.hpp) with its face tables in LDS
-template <bool G3D, bool OBL, int WPE, bool FLOW = false>
+// k_trace (kernel_trace.hpp) with its face tables -- and, KL, the per-cell extinction and
+// albedo -- in LDS
+template <bool G3D, bool OBL, int WPE, bool FLOW = false, bool KL = false>
 static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L, hipStream_t stream) {
-    const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
-    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW>, lds);
+    const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi) + (KL ? trace_ka_bytes(G.ncell) : 0);
+    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW, KL>, lds);
     g->trace_blocks = round_sub(per_cu * g->num_cus);
     timed(g, ARTES_K_TRACE, stream, [&] {
-        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW, KL>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
+}
+
+// the per-cell table in LDS for k_trace when it is small (ARTES_KLDS=0 turns it off)
+static bool use_klds(const DevGrid& G) {
+    const char* e = getenv("ARTES_KLDS");
+    // (and the block's LDS stays small enough for 4 blocks per CU: 160 KiB / 4, less the queues)
+    return (e ? atoi(e) != 0 : true) && trace_ka_bytes(G.ncell) <= KL_MAX_BYTES &&
+           trace_table_bytes(G.nr, G.ntheta, G.nphi) + trace_ka_bytes(G.ncell) <= 36864;
 }
 
 // k_trace variant: 3D or radial-only grid, spheroidal (oblate) or spherical planet,
@@ -354,10 +365,12 @@ static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, 
         if (oblate) launch_trace<G3D, true, 4, true>(g, bpc, G, R, L, stream);
         else launch_trace<G3D, false, 4, true>(g, bpc, G, R, L, stream);
     } else if (oblate) {
-        if (wpe == 3) launch_trace<G3D, true, 3>(g, bpc, G, R, L, stream);
+        if (use_klds(G)) launch_trace<G3D, true, 4, false, true>(g, bpc, G, R, L, stream);
+        else if (wpe == 3) launch_trace<G3D, true, 3>(g, bpc, G, R, L, stream);
         else launch_trace<G3D, true, 4>(g, bpc, G, R, L, stream);
     } else {
-        if (wpe == 3) launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
+        if (use_klds(G)) launch_trace<G3D, false, 4, false, true>(g, bpc, G, R, L, stream);
+        else if (wpe == 3) launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
         else launch_trace<G3D, false, 4>(g, bpc, G, R, L, stream);
     }
 }
@@ -372,9 +385,9 @@ static void dump_live(artes_grid* g, const int* cnt, int in, hipStream_t stream)
     if (hipStreamSynchronize(stream) != hipSuccess) return;
     for (int s = 0; s < NSUB; s++) {
         fprintf(stderr, "[artes] sub-engine %d: live trace list %d entries (split %d)\n", s, n[s], split[s]);
-        const int* d_list = g->d_lists[in] + (size_t)s * Ps;
+        const int* d_list = g->d_lists[in] + (size_t)s * 2 * Ps;
         for (int j = 0; j < n[s] && j < 2; j++) {
-            const int pos = j < split[s] ? j : Ps - 1 - (j - split[s]);
+            const int pos = j < split[s] ? j : 2 * Ps - 1 - (j - split[s]);
             int slot = -1;
             Slot r;
             SlotDiag q;
@@ -456,15 +469,15 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         SubLists SL;
         for (int s = 0; s < NSUB; s++) {
             Lists& L = SL.l[s];
-            const size_t o = (size_t)s * Ps;
-            L.trace_in = g->d_lists[in] + o; L.trace_in_n = cnt + (CNT_IN0 + in) * NSUB + s;
+            const size_t o = (size_t)s * Ps, ot = (size_t)s * 2 * Ps;
+            L.trace_in = g->d_lists[in] + ot; L.trace_in_n = cnt + (CNT_IN0 + in) * NSUB + s;
             L.trace_in_split = cnt + (CNT_SPLIT0 + in) * NSUB + s;
-            L.trace_out = g->d_lists[1 - in] + o; L.trace_out_n = cnt + (CNT_IN0 + 1 - in) * NSUB + s;
+            L.trace_out = g->d_lists[1 - in] + ot; L.trace_out_n = cnt + (CNT_IN0 + 1 - in) * NSUB + s;
             L.event = g->d_event + o; L.event_n = cnt + CNT_EVENT * NSUB + s;
             L.emit = g->d_emit + o; L.emit_n = cnt + CNT_EMIT * NSUB + s;
             L.grab = g->d_grab + 8 * s; L.next_pkt = g->d_next + s;
             L.dbg_owner = g->d_owner; L.dbg_iter = cnt + CNT_DBG * NSUB + s;
-            L.P = Ps; L.first = sub_first[s]; L.n = sub_n[s];
+            L.P = 2 * Ps; L.first = sub_first[s]; L.n = sub_n[s];
         }
         return SL;
     };
@@ -483,7 +496,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         SubLists L = lists(1);   // trace_out = list 0
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
-            hipLaunchKernelGGL(k_rotate, dim3(NSUB), dim3(64), 0, stream, cnt, 1, g->d_grab, g->d_next, R.emit_first, Ps, R.err);
+            hipLaunchKernelGGL(k_rotate, dim3(NSUB), dim3(64), 0, stream, cnt, 1, g->d_grab, g->d_next, R.emit_first, 2 * Ps, R.err);
         });
     }
     HIP_TRY(hipGetLastError());
@@ -508,7 +521,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         });
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
-            hipLaunchKernelGGL(k_rotate, dim3(NSUB), dim3(64), 0, stream, cnt, in, g->d_grab, g->d_next, R.emit_first, Ps, R.err);
+            hipLaunchKernelGGL(k_rotate, dim3(NSUB), dim3(64), 0, stream, cnt, in, g->d_grab, g->d_next, R.emit_first, 2 * Ps, R.err);
         });
         in = 1 - in;
         it++;

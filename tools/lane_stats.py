@@ -1,5 +1,7 @@
 """Lane occupancy of k_trace (needs the -DARTES_DEBUG_LANES build via ARTES_LIB_PATH).
-usage: python tools/lane_stats.py [packets] [ENV=VAL,ENV=VAL ...]  (one variant per argument)"""
+usage: python tools/lane_stats.py [packets] [ENV=VAL,ENV=VAL ...]  (one variant per argument)
+LS_WORKLOAD=cloudy: the configs[3] cloudy atmosphere (synthetic.make_cloudy, 0.45 micron, the
+`phase` mode's 1-pixel detector at 0 degrees) instead of ray3d."""
 import os
 import sys
 
@@ -10,12 +12,19 @@ from artes_amd.engine import Grid  # noqa: E402
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 5 * 10**7
 variants = [dict(kv.split("=", 1) for kv in v.split(",")) if v else {} for v in (sys.argv[2:] or [""])]
 cfg = driver.default_config()
-for name in ("ray3d",):
-    atm = synthetic.make_config(name, share_matrix=True)
+for name in (os.environ.get("LS_WORKLOAD", "ray3d"),):
+    if name == "cloudy":
+        import tempfile
+
+        atm = synthetic.make_cloudy(os.path.join(tempfile.mkdtemp(), "cloudy"), wavelength=(0.45,))
+        cfg.apply("detector:type", "phase")
+    else:
+        atm = synthetic.make_config(name, share_matrix=True)
     det = driver.detector_geometry(cfg, atm["radial"][-1])
     g = Grid(atm, 0)
     g.set_profiling(True)
-    p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0))
+    p = driver.run_params(cfg, det, 0, det_phi=1e-5 if name == "cloudy" else None, cell_depth=g.cell_depth(0),
+                          packet_moments=False)
     for env in variants:
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)

@@ -8,7 +8,8 @@ fabric bytes = 2 FETCH_SIZE + WRITE_SIZE KiB (the gfx950 FETCH_SIZE correction),
 TCC_HIT / (TCC_HIT + TCC_MISS), VALU / SALU busy = 4 SQ_INSTS_* / (GRBM_GUI_ACTIVE / 8 x 1024
 SIMDs), the wave-cycle split issuing / waiting on memory / issue-stalled, LDS bank-conflict
 share of LDS cycles; per scattering event (k_event) and per crossing (k_trace) from the
-engine counters of the profiled calls."""
+engine counters of the profiled calls.  A counter collected in more than one pass is
+averaged over those passes."""
 import csv
 import glob
 import hashlib
@@ -18,11 +19,14 @@ import sys
 from collections import defaultdict
 
 SIMDS = 256 * 4
-tot = defaultdict(lambda: defaultdict(float))
+# a counter collected in several passes (GRBM_GUI_ACTIVE rides along in three) is averaged
+# over them, not summed: each pass profiles the same command
+per_pass = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
 for f in sorted(glob.glob(os.path.join(sys.argv[1], "*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("artes::", "")
-        tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        per_pass[k][r["Counter_Name"]][f] += float(r["Counter_Value"])
+tot = {k: {c: sum(v.values()) / len(v) for c, v in cs.items()} for k, cs in per_pass.items()}
 runs = json.load(open(sys.argv[2]))
 calls = [c for key in ("phase", "spectrum") for c in runs.get(key, [])]
 packets = sum(c["packets"] for c in calls)
