@@ -124,18 +124,11 @@ struct TraceTabs {
     const FaceRec* fr;
     const double2* phsc;
     const double2* tcs;   // (cos, sin)(theta_k), for the set-up bounds
-    const double2* ka;    // KL: the (extinction, albedo) pairs of this wavelength, [ncell]
 };
 
 __host__ __device__ inline size_t trace_table_bytes(int nr, int ntheta, int nphi) {
     return sizeof(FaceRec) * ((size_t)(nr + 1) + (size_t)(ntheta + 1)) + sizeof(double2) * ((size_t)nphi + ntheta + 1);
 }
-// with the per-cell (extinction, albedo) table in LDS too (KL): small grids -- the cloudy and
-// thermal atmospheres of configs[3] / configs[4], the radial-only ones of configs[0] / [1]
-__host__ __device__ inline size_t trace_ka_bytes(int ncell) { return sizeof(double2) * (size_t)ncell; }
-constexpr size_t KL_MAX_BYTES = 32768;
-
-template <bool KL = false>
 __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double* lds) {
     TraceTabs T;
     FaceRec* fr = (FaceRec*)lds;
@@ -155,13 +148,8 @@ __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double
         const double c = G.tcos[i];
         tcs[i] = make_double2(c, sqrt(fmax(0.0, 1.0 - c * c)));
     }
-    double2* ka = tcs + (G.ntheta + 1);
-    if constexpr (KL) {
-        const double2* src = (const double2*)G.ka;
-        for (int i = threadIdx.x; i < G.ncell; i += BLOCK) ka[i] = src[i];
-    }
     __syncthreads();
-    T.fr = fr; T.phsc = phsc; T.tcs = tcs; T.ka = ka;
+    T.fr = fr; T.phsc = phsc; T.tcs = tcs;
     return T;
 }
 
@@ -430,14 +418,11 @@ __device__ __noinline__ void flow_segment(double* flow_g, double* flow_t, int ce
 // the other two.  The linear cell index is updated with the crossing, not recomputed.
 //
 // FLOW instantiations add the energy-transport diagnostics to propagation segments.
-//
-// KL instantiations read the (extinction, albedo) pair of a cell from an LDS copy of the
-// wavelength's table (grids of up to KL_MAX_BYTES / 16 cells) instead of global memory.
-template <bool G3D, bool OBL, int WPE, bool FLOW = false, bool KL = false>
+template <bool G3D, bool OBL, int WPE, bool FLOW = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G, DevRun R, Pool S, SubLists SL) {
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_tab[];
-    const TraceTabs T = stage_trace_tables<KL>(G, s_tab);
+    const TraceTabs T = stage_trace_tables(G, s_tab);
     const int n = *L.trace_in_n;
     const int split = *L.trace_in_split;   // [0, split): new packets' traces; then k_event's, stored backwards
     const int home = sub_block() & 7;
@@ -484,9 +469,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             cell = 0;
         }
 #endif
-        double2 kv;
-        if constexpr (KL) kv = T.ka[cell];
-        else kv = *(const double2*)((const char*)G.ka + ((unsigned)cell << 4));
+        const double2 kv = *(const double2*)((const char*)G.ka + ((unsigned)cell << 4));
         kext = kv.x;
         alb = kv.y;
     };

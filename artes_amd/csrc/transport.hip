@@ -335,24 +335,18 @@ static int32_t ensure_pool(artes_grid* g, uint64_t n) {
 // grids are whole multiples of the sub-engine count (block b works on sub-engine b % NSUB)
 static int round_sub(int blocks) { return std::max(NSUB, (blocks + NSUB - 1) / NSUB * NSUB); }
 
-// k_trace (kernel_trace.hpp) with its face tables -- and, KL, the per-cell extinction and
-// albedo -- in LDS
-template <bool G3D, bool OBL, int WPE, bool FLOW = false, bool KL = false>
+// k_trace (kernel_trace.hpp) with its face tables in LDS.  (The per-cell extinction and
+// albedo in LDS as well, for grids whose table fits, measured the same as reading them from
+// L2 -- cloudy 210.8 vs 211.1, hg 705 vs 707 Mpackets/s, profiles/r03/klds_ab.txt -- so they
+// stay in global memory.)
+template <bool G3D, bool OBL, int WPE, bool FLOW = false>
 static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L, hipStream_t stream) {
-    const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi) + (KL ? trace_ka_bytes(G.ncell) : 0);
-    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW, KL>, lds);
+    const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
+    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW>, lds);
     g->trace_blocks = round_sub(per_cu * g->num_cus);
     timed(g, ARTES_K_TRACE, stream, [&] {
-        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW, KL>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
-}
-
-// the per-cell table in LDS for k_trace when it is small (ARTES_KLDS=0 turns it off)
-static bool use_klds(const DevGrid& G) {
-    const char* e = getenv("ARTES_KLDS");
-    // (and the block's LDS stays small enough for 4 blocks per CU: 160 KiB / 4, less the queues)
-    return (e ? atoi(e) != 0 : true) && trace_ka_bytes(G.ncell) <= KL_MAX_BYTES &&
-           trace_table_bytes(G.nr, G.ntheta, G.nphi) + trace_ka_bytes(G.ncell) <= 36864;
 }
 
 // k_trace variant: 3D or radial-only grid, spheroidal (oblate) or spherical planet,
@@ -365,12 +359,10 @@ static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, 
         if (oblate) launch_trace<G3D, true, 4, true>(g, bpc, G, R, L, stream);
         else launch_trace<G3D, false, 4, true>(g, bpc, G, R, L, stream);
     } else if (oblate) {
-        if (use_klds(G)) launch_trace<G3D, true, 4, false, true>(g, bpc, G, R, L, stream);
-        else if (wpe == 3) launch_trace<G3D, true, 3>(g, bpc, G, R, L, stream);
+        if (wpe == 3) launch_trace<G3D, true, 3>(g, bpc, G, R, L, stream);
         else launch_trace<G3D, true, 4>(g, bpc, G, R, L, stream);
     } else {
-        if (use_klds(G)) launch_trace<G3D, false, 4, false, true>(g, bpc, G, R, L, stream);
-        else if (wpe == 3) launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
+        if (wpe == 3) launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
         else launch_trace<G3D, false, 4>(g, bpc, G, R, L, stream);
     }
 }
