@@ -476,7 +476,7 @@ struct TabLayout {
 
 // one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended); the peel
 // contribution goes to `D` (see DetAcc)
-template <bool PIX1, bool PAD>
+template <bool PIX1, bool PAD, bool PADC = PAD>
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, const Line0& L0,
                                          DetAcc<PIX1>& D, uint32_t& c_scat, uint32_t& c_det) {
     {
@@ -498,7 +498,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         unpack_cell(L0.pcell, cr, ct, cp);
         const int cell = cr + G.nr * (ct + G.ntheta * cp);
         const int mid = G.nmat == 1 ? 0 : G.matid[cell];   // uniform atmosphere: no dependent load
-        using TL = TabLayout<PAD>;
+        using TL = TabLayout<PAD>;     // the matrices
+        using TC = TabLayout<PADC>;    // the cumulative sampling tables
         const double* __restrict__ P = G.mats + (size_t)mid * TL::MAT;
         const double tau_peel = L0.tpeel;
         bool drop = false;
@@ -585,7 +586,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         if (R.rec) S.d[slot].nscat += 1;
         Rng rng; rng.s0 = L0.r0; rng.s1 = L0.r1;
         double alpha, beta;
-        sample_angles<TL::CS>(G, R, G.cums + (size_t)mid * TL::CUM, rng, st, alpha, beta);
+        sample_angles<TC::CS>(G, R, G.cums + (size_t)mid * TC::CUM, rng, st, alpha, beta);
         double e0, e1, e2;
         direction_cosine(R, alpha, beta, dx, dy, dz, e0, e1, e2);
         double sc[16];
@@ -615,6 +616,10 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
 __host__ __device__ inline size_t event_table_doubles(int nmat) {
     return (size_t)nmat * (TabLayout<true>::MAT + TabLayout<true>::CUM) + 2 * (NANG + 1);
 }
+// the same for the cumulative tables and the azimuth tables alone (LDS_C)
+__host__ __device__ inline size_t event_cum_doubles(int nmat) {
+    return (size_t)nmat * TabLayout<true>::CUM + 2 * (NANG + 1);
+}
 
 // peel-off contribution + scattering (ARTES.f90:4765-4984, 819-846).
 //  LDS_T: the scattering tables (one 31 KB set per distinct matrix) are staged in LDS --
@@ -629,14 +634,32 @@ __host__ __device__ inline size_t event_table_doubles(int nmat) {
 #endif
 //  PIX1:  a one-pixel detector: per-lane sums in LDS slots after the tables, reduced over
 //         the wave at the end (DetAcc); no LDS detector then.
-template <bool LDS_T, bool LDS_D, bool PIX1 = false, int EB = BLOCK>
+//  LDS_C: (without LDS_T) the matrices too many for LDS -- the cloudy atmospheres, ~9 per
+//         wavelength at 23 KB each -- but their cumulative tables and the azimuth tables
+//         (7.2 KB per matrix) staged: the two 4-ary searches, 8 dependent table reads per
+//         event, then wait on LDS, and only the interpolation's independent row reads go to
+//         L2.  (The call's matrices are its wavelength's only: the host remaps matrix ids
+//         per wavelength, transport.hip, wl_set.)
+template <bool LDS_T, bool LDS_D, bool PIX1 = false, int EB = BLOCK, bool LDS_C = false>
 __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, SubLists SL) {
     static_assert(!(PIX1 && LDS_D), "a one-pixel detector is reduced per lane");
+    static_assert(!(LDS_T && LDS_C), "LDS_C stages the cumulative tables alone");
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_ev[];
     DevGrid G = G0;
     const size_t plane = (size_t)R.nx * R.ny;
     double* lds_next = s_ev;
+    if constexpr (LDS_C) {
+        using TL = TabLayout<true>;
+        const int nc = G0.nmat * CUM_DOUBLES;
+        double* c = s_ev;
+        double* a = c + G0.nmat * TL::CUM;
+        double* b = a + (NANG + 1);
+        for (int i = threadIdx.x; i < nc; i += EB) c[(i >> 2) * TL::CS + (i & 3)] = G0.cums[i];    // entries of 4 -> 5
+        for (int i = threadIdx.x; i <= NANG; i += EB) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
+        G.cums = c; G.sc2 = a; G.ss2 = b;
+        lds_next = b + (NANG + 1);
+    }
     if constexpr (LDS_T) {
         using TL = TabLayout<true>;
         const int nm = G0.nmat * MAT_DOUBLES, nc = G0.nmat * CUM_DOUBLES;
@@ -656,7 +679,7 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         acc = lds_next;
         for (size_t i = threadIdx.x; i < 9 * plane; i += EB) acc[i] = 0.0;
     }
-    if constexpr (LDS_T || LDS_D) __syncthreads();
+    if constexpr (LDS_T || LDS_D || LDS_C) __syncthreads();
     DetAcc<PIX1> D;
     D.init(det, acc, plane, lds_next, EB);
     const int n = *L.event_n;
@@ -678,7 +701,7 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
 #ifdef ARTES_DEBUG
         if (i < n) dbg_claim(R, L, slot, S.P, 1, slot >= 0 && to_event_list(cur.mode));
 #endif
-        const int dest = slot >= 0 ? event_one<PIX1, LDS_T>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
+        const int dest = slot >= 0 ? event_one<PIX1, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
 #ifdef ARTES_DEBUG

@@ -106,6 +106,15 @@ struct artes_grid {
     long long last_iterations = 0;
     // occupancy answers per (kernel, dynamic LDS bytes), queried once per grid
     std::vector<std::pair<std::pair<const void*, size_t>, int>> occ;
+    // the scattering matrices of one wavelength, renumbered (wl_set): a call reads only its
+    // wavelength's matrices, so k_event's LDS budget is spent on those alone
+    struct WlSet {
+        int nmat = -1;
+        double* d_mats = nullptr;   // [nmat][180][16]
+        double* d_cums = nullptr;   // [nmat][181][4]
+        int* d_matid = nullptr;     // [ncell] local ids
+    };
+    std::vector<WlSet> wl;
     // per-launch timing (artes_set_profiling)
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;     // start/end pairs
@@ -195,6 +204,11 @@ void artes_grid_destroy(artes_grid* g) {
                      g->d_owner};
     for (void* p : eptrs)
         if (p) hipFree(p);
+    for (auto& W : g->wl) {
+        if (W.d_mats) hipFree(W.d_mats);
+        if (W.d_cums) hipFree(W.d_cums);
+        if (W.d_matid) hipFree(W.d_matid);
+    }
     if (g->h_count) hipHostFree(g->h_count);
     if (g->ev_poll) hipEventDestroy(g->ev_poll);
     for (hipEvent_t e : g->prof_ev) hipEventDestroy(e);
@@ -229,9 +243,6 @@ int32_t artes_grid_create(const artes_grid_desc* desc, int32_t device, artes_gri
         for (size_t i = 0; i < T.kappa.size(); i++) { ka[2 * i] = T.kappa[i]; ka[2 * i + 1] = T.albedo[i]; }
         HIP_TRY(upload(&g->d_ka, ka));
     }
-    HIP_TRY(upload(&g->d_matid, T.matid));
-    HIP_TRY(upload(&g->d_mats, T.mats));
-    HIP_TRY(upload(&g->d_cums, T.cums));
     HIP_TRY(upload(&g->d_sc2, T.sc2));
     HIP_TRY(upload(&g->d_ss2, T.ss2));
     HIP_TRY(upload(&g->d_rfront, T.rfront));
@@ -276,6 +287,35 @@ int32_t artes_grid_thermal(artes_grid* g, int32_t wl, int32_t thermal_weight, in
 }
 
 }  // extern "C"
+
+// the matrices wavelength `wl` uses, renumbered in order of first use over the cells, with
+// their cumulative tables and the per-cell local ids (built on the first call at `wl`)
+static int32_t wl_set(artes_grid* g, int wl, artes_grid::WlSet** out) {
+    if (g->wl.empty()) g->wl.resize(g->T.nwav);
+    artes_grid::WlSet& W = g->wl[wl];
+    if (W.nmat < 0) {
+        const HostTables& T = g->T;
+        const size_t nc = (size_t)T.ncell;
+        std::vector<int> loc((size_t)T.nmat, -1), ids;
+        std::vector<int32_t> matid(nc);
+        for (size_t c = 0; c < nc; c++) {
+            const int gid = T.matid[(size_t)wl * nc + c];
+            if (loc[gid] < 0) { loc[gid] = (int)ids.size(); ids.push_back(gid); }
+            matid[c] = loc[gid];
+        }
+        std::vector<double> mats(ids.size() * MAT_DOUBLES), cums(ids.size() * CUM_DOUBLES);
+        for (size_t k = 0; k < ids.size(); k++) {
+            std::memcpy(&mats[k * MAT_DOUBLES], &T.mats[(size_t)ids[k] * MAT_DOUBLES], MAT_DOUBLES * sizeof(double));
+            std::memcpy(&cums[k * CUM_DOUBLES], &T.cums[(size_t)ids[k] * CUM_DOUBLES], CUM_DOUBLES * sizeof(double));
+        }
+        HIP_TRY(upload(&W.d_mats, mats));
+        HIP_TRY(upload(&W.d_cums, cums));
+        HIP_TRY(upload(&W.d_matid, matid));
+        W.nmat = (int)ids.size();
+    }
+    *out = &W;
+    return 0;
+}
 
 static bool use_event_engine() {
     const char* e = getenv("ARTES_ENGINE");
@@ -422,19 +462,29 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     // (k_event PIX1) instead of same-address atomics; ARTES_PIX1=0 turns it off
     const char* p1 = getenv("ARTES_PIX1");
     const bool pix1 = (p1 ? atoi(p1) != 0 : true) && R.nx == 1 && R.ny == 1;
-    const char* dl = getenv("ARTES_DET_LDS");
-    const bool det_lds = !pix1 && (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
     // k_event's block with both the tables and the detector in LDS: 768 threads, one block
     // (12 waves, 3 per SIMD at <= 170 VGPRs) per CU sharing one LDS copy, instead of two
     // 256-thread blocks (2 waves per SIMD, LDS-bound): k_event -7 % on ray3d / hg / iso
     // (ARTES_EVENT_BLOCK=256 for the old shape)
     const char* ebs = getenv("ARTES_EVENT_BLOCK");
     const int ev_block = ebs && atoi(ebs) == 256 ? 256 : 768;
+    // matrices too many for LDS: their cumulative tables alone in LDS (k_event LDS_C) when
+    // they fit beside the detector or the one-pixel lane slots in one 768-thread block per
+    // CU; ARTES_EVENT_LDSC=0 turns it off
+    const char* elc = getenv("ARTES_EVENT_LDSC");
+    const size_t cum_bytes = event_cum_doubles(G.nmat) * sizeof(double);
+    const bool ev_ldsc_ok = !ev_lds && ev_block == 768 && (elc ? atoi(elc) != 0 : true);
+    const char* dl = getenv("ARTES_DET_LDS");
+    const bool det_lds = !pix1 && (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
+    const size_t lds_cap = 160 * 1024 - 4096;   // (a margin for static LDS)
+    const bool ev_ldsc = ev_ldsc_ok && cum_bytes + (pix1 ? pix1_slot_bytes(768) : det_lds ? det_bytes : 0) <= lds_cap;
+    const size_t tab_bytes = ev_lds ? ev_bytes : (ev_ldsc ? cum_bytes : 0);
     int ev_blocks = side_blocks;
     if (det_lds) {
-        const size_t b = (ev_lds ? ev_bytes : 0) + det_bytes;
+        const size_t b = tab_bytes + det_bytes;
         int per_cu = ev_block == 768 ? (ev_lds ? blocks_per_cu(g, k_event<true, true, false, 768>, b, 768)
-                                               : blocks_per_cu(g, k_event<false, true, false, 768>, b, 768))
+                                               : ev_ldsc ? blocks_per_cu(g, k_event<false, true, false, 768, true>, b, 768)
+                                                         : blocks_per_cu(g, k_event<false, true, false, 768>, b, 768))
                                      : (ev_lds ? blocks_per_cu(g, k_event<true, true>, b) : blocks_per_cu(g, k_event<false, true>, b));
         const char* eb = getenv("ARTES_EVENT_BPC");
         if (eb) per_cu = std::max(1, atoi(eb));
@@ -443,12 +493,16 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     // the one-pixel kernel in 768-thread blocks too: the launch bound holds it to 3 waves per
     // SIMD (<= 168 VGPRs; 211-219 at 256 threads, i.e. 2 waves)
     const bool pix1_768 = pix1 && ev_block == 768;
-    const size_t p1_bytes = (ev_lds ? ev_bytes : 0) + pix1_slot_bytes(pix1_768 ? 768 : BLOCK);
+    const size_t p1_bytes = tab_bytes + pix1_slot_bytes(pix1_768 ? 768 : BLOCK);
     if (pix1_768) {
         const int per_cu = ev_lds ? blocks_per_cu(g, k_event<true, false, true, 768>, p1_bytes, 768)
-                                  : blocks_per_cu(g, k_event<false, false, true, 768>, p1_bytes, 768);
+                                  : ev_ldsc ? blocks_per_cu(g, k_event<false, false, true, 768, true>, p1_bytes, 768)
+                                            : blocks_per_cu(g, k_event<false, false, true, 768>, p1_bytes, 768);
         ev_blocks = round_sub(per_cu * g->num_cus);
     }
+    // the global-detector kernel with LDS_C: one 768-thread block per CU as well
+    const bool glob_ldsc = ev_ldsc && !pix1 && !det_lds;
+    if (glob_ldsc) ev_blocks = round_sub(blocks_per_cu(g, k_event<false, false, false, 768, true>, cum_bytes, 768) * g->num_cus);
     // the packet ids of the call split into NSUB contiguous ranges, one per sub-engine
     const uint64_t chunk = (R.n + NSUB - 1) / NSUB;
     uint64_t sub_first[NSUB], sub_n[NSUB];
@@ -501,6 +555,9 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         launch_trace_any<G3D>(g, wpe, trace_bpc, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
             if (pix1_768 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true, 768>), dim3(ev_blocks), dim3(768), p1_bytes, stream, G, R, g->pool, L);
+            else if (pix1_768 && ev_ldsc) hipLaunchKernelGGL((k_event<false, false, true, 768, true>), dim3(ev_blocks), dim3(768), p1_bytes, stream, G, R, g->pool, L);
+            else if (det_lds && ev_ldsc) hipLaunchKernelGGL((k_event<false, true, false, 768, true>), dim3(ev_blocks), dim3(768), cum_bytes + det_bytes, stream, G, R, g->pool, L);
+            else if (glob_ldsc) hipLaunchKernelGGL((k_event<false, false, false, 768, true>), dim3(ev_blocks), dim3(768), cum_bytes, stream, G, R, g->pool, L);
             else if (pix1_768) hipLaunchKernelGGL((k_event<false, false, true, 768>), dim3(ev_blocks), dim3(768), p1_bytes, stream, G, R, g->pool, L);
             else if (pix1 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L);
             else if (pix1) hipLaunchKernelGGL((k_event<false, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L);
@@ -538,8 +595,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     }
     g->last_iterations = it;
     if (getenv("ARTES_VERBOSE"))
-        fprintf(stderr, "[artes] event engine: pool %d, %lld iterations, trace blocks %d, event blocks %d (LDS tables %d, detector %d, 1-pixel %d)\n",
-                P, it, g->trace_blocks, ev_blocks, (int)ev_lds, (int)det_lds, (int)pix1);
+        fprintf(stderr, "[artes] event engine: pool %d, %lld iterations, trace blocks %d, event blocks %d (LDS tables %d, cumulative tables %d, detector %d, 1-pixel %d, matrices %d)\n",
+                P, it, g->trace_blocks, ev_blocks, (int)ev_lds, (int)ev_ldsc, (int)det_lds, (int)pix1, G.nmat);
     return 0;
 }
 
@@ -604,8 +661,13 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     G.kappa = g->d_kappa + (size_t)p->wl_index * T.ncell;
     G.albedo = g->d_albedo + (size_t)p->wl_index * T.ncell;
     G.ka = g->d_ka + 2 * (size_t)p->wl_index * T.ncell;
-    G.matid = g->d_matid + (size_t)p->wl_index * T.ncell;
-    G.mats = g->d_mats; G.cums = g->d_cums; G.sc2 = g->d_sc2; G.ss2 = g->d_ss2;
+    {
+        artes_grid::WlSet* W = nullptr;
+        const int32_t rc = wl_set(g, p->wl_index, &W);
+        if (rc) return rc;
+        G.nmat = W->nmat; G.matid = W->d_matid; G.mats = W->d_mats; G.cums = W->d_cums;
+    }
+    G.sc2 = g->d_sc2; G.ss2 = g->d_ss2;
 
     DevRun R;
     R.first = first; R.n = n; R.seed = seed;
@@ -619,7 +681,9 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // refill a wave once this many of its lanes are idle (re-swept after the batched
     // interactions: 16 on 3D grids, 20 on radial-only ones)
     const bool grid3d = (T.ntheta > 1 || T.nphi > 1);
-    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? 16 : 20);
+    // (coarse 3D grids -- the cloudy atmospheres of configs[3], ~600 cells -- have short traces
+    // and refill best at 32: cloudy phase +2.7 %, spectrum +4 %, profiles/r03/cloudy_ldsc_refill.txt)
+    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? (T.ncell < 4096 ? 32 : 16) : 20);
     const char* ef = getenv("ARTES_EMIT_FIRST");
     R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
     const char* bw = getenv("ARTES_BACKWARD");
