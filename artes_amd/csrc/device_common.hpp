@@ -290,9 +290,13 @@ __device__ __forceinline__ void mueller(double psi, double& c2p, double& s2p) {
         s2p = -s2p;
 }
 
-// polarization_rotation (ARTES.f90:1663-1932); sc is scatter(4,4) row-major
+// polarization_rotation (ARTES.f90:1663-1932); sc is scatter(4,4) row-major.  c2b / s2b:
+// mueller(beta), when the caller has it already (the scattering path: sample_angles computed
+// it for the same beta), else computed here (HAVE_CS = false)
+template <bool HAVE_CS = false>
 __device__ void polarization_rotation(const DevRun& R, double alpha, double beta, const double si[4],
-                                      const double sc[16], double d2, double dn2, double so[4], bool peeling) {
+                                      const double sc[16], double d2, double dn2, double so[4], bool peeling,
+                                      double c2b = 0.0, double s2b = 0.0) {
     if (fabs(alpha) < 1.0 && fabs(dn2) < 1.0) {
         double beta2 = 0.0;
         const double num = (d2 - dn2 * alpha) / (dsqrt(1.0 - alpha * alpha) * dsqrt(1.0 - dn2 * dn2));
@@ -300,8 +304,8 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
         else if (num > 1.0 && num < 1.00001) beta2 = 0.0;
         else if (num < -1.0 && num > -1.00001) beta2 = PI;
         else log_err(R, 11);
-        double c, s;
-        mueller(beta, c, s);
+        double c = c2b, s = s2b;
+        if constexpr (!HAVE_CS) mueller(beta, c, s);
         double r0 = si[0], r1 = c * si[1] + s * si[2], r2 = -s * si[1] + c * si[2], r3 = si[3];
         const double pr = dsqrt(r1 * r1 + r2 * r2 + r3 * r3);
         double norm = (pr > 0.0) ? dsqrt(si[1] * si[1] + si[2] * si[2] + si[3] * si[3]) / pr : 1.0;
@@ -351,13 +355,21 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
     }
 }
 
-// direction_cosine (ARTES.f90:1962-2052)
+// the azimuth of direction (d0, d1) in [0, 2 pi) as direction_cosine takes it (ARTES.f90:1975-1977)
+__device__ __forceinline__ double azimuth(double d0, double d1) {
+    double phi = atan2(d1, d0);
+    if (phi < 0.0) phi += TWO_PI;
+    return phi;
+}
+
+// direction_cosine (ARTES.f90:1962-2052); phi_old = azimuth(d0, d1), when the caller has it
+// already (k_event: the peel-off needed the same azimuth), else computed here
+template <bool HAVE_PHI = false>
 __device__ void direction_cosine(const DevRun& R, double alpha, double beta, double d0, double d1, double d2,
-                                 double& e0, double& e1, double& e2) {
+                                 double& e0, double& e1, double& e2, double phi_in = 0.0) {
     const double cto = d2 / dsqrt(d0 * d0 + d1 * d1 + d2 * d2);
     const double sto = dsqrt(1.0 - cto * cto);
-    double phi_old = atan2(d1, d0);
-    if (phi_old < 0.0) phi_old += TWO_PI;
+    const double phi_old = HAVE_PHI ? phi_in : azimuth(d0, d1);
     double ctn = 0.0, phi_new = 0.0, spn = 0.0;
     const bool upper = (beta >= PI && beta < TWO_PI);
     const bool lower = (beta >= 0.0 && beta < PI);
@@ -451,7 +463,7 @@ __device__ __forceinline__ int cdf_search4(double s, F cdf) {
 // C = [181][CS] (CS = 4, or 5 in LDS: see k_event)
 template <int CS = 4>
 __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* __restrict__ C, Rng& rng,
-                              const double st[4], double& alpha, double& beta) {
+                              const double st[4], double& alpha, double& beta, double& c2b, double& s2b) {
     // azimuth: C_b(i) = i (p11 I + p14 V) + (p12 Q + p13 U) SC2(i) + (p12 U - p13 Q) SS2(i)
     const double p11 = C[180 * CS + 0], p12 = C[180 * CS + 1], p13 = C[180 * CS + 2], p14 = C[180 * CS + 3];
     const double u = p11 * st[0] + p14 * st[3];
@@ -466,7 +478,6 @@ __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* _
     if (rng.uni() > 0.5) beta = beta + PI;
     if (beta >= TWO_PI) beta = TWO_PI - 1.e-10;
     if (beta <= 0.0) beta = -TWO_PI + 1.e-10;
-    double c2b, s2b;
     mueller(beta, c2b, s2b);
     // polar: C_t(i) = I A1(i) + (c2b Q + s2b U) A2(i) + (c2b U - s2b Q) A3(i) + V A4(i)
     const double k0 = st[0], k1 = c2b * st[1] + s2b * st[2], k2 = c2b * st[2] - s2b * st[1], k3 = st[3];

@@ -502,6 +502,9 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         using TC = TabLayout<PADC>;    // the cumulative sampling tables
         const double* __restrict__ P = G.mats + (size_t)mid * TL::MAT;
         const double tau_peel = L0.tpeel;
+        // the incoming direction's azimuth: the peel-off's phi_old (ARTES.f90:4868-4870) and the
+        // scattering's (direction_cosine, 1975-1977) -- one atan2 for both
+        const double phi_old = azimuth(dx, dy);
         bool drop = false;
         if ((m & FLAG_EXIT) && tau_peel < 50.0) {
             const double w = exp(-tau_peel);
@@ -510,9 +513,6 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             else if (mu <= -1.0) mu = -1.0 + 1.e-10;
             double sc[16];
             interp_matrix<TL::RS>(P, acos(mu), sc);
-            double phi_old = atan2(dy, dx);
-            if (phi_old < 0.0) phi_old += TWO_PI;
-            if (phi_old > TWO_PI) phi_old -= TWO_PI;
             const double phi_new = R.det_phi;   // the detector's azimuth, once per run
             bool have_out = false;
             double so[4] = {0, 0, 0, 0};
@@ -585,15 +585,15 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         c_scat++;
         if (R.rec) S.d[slot].nscat += 1;
         Rng rng; rng.s0 = L0.r0; rng.s1 = L0.r1;
-        double alpha, beta;
-        sample_angles<TC::CS>(G, R, G.cums + (size_t)mid * TC::CUM, rng, st, alpha, beta);
+        double alpha, beta, c2b, s2b;
+        sample_angles<TC::CS>(G, R, G.cums + (size_t)mid * TC::CUM, rng, st, alpha, beta, c2b, s2b);
         double e0, e1, e2;
-        direction_cosine(R, alpha, beta, dx, dy, dz, e0, e1, e2);
+        direction_cosine<true>(R, alpha, beta, dx, dy, dz, e0, e1, e2, phi_old);
         double sc[16];
         interp_matrix<TL::RS>(P, acos(alpha), sc);
         if (fabs(alpha) < 1.0) {
             double sn[4];
-            polarization_rotation(R, alpha, beta, st, sc, dz, e2, sn, false);
+            polarization_rotation<true>(R, alpha, beta, st, sc, dz, e2, sn, false, c2b, s2b);
             const double inv = sn[0] != 0.0 ? 1.0 / sn[0] : 0.0;
             S.s[slot].q1 = sn[1] * inv; S.s[slot].q2 = sn[2] * inv; S.s[slot].q3 = sn[3] * inv;
             S.s[slot].wI = sn[0];

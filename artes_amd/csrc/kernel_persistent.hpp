@@ -185,7 +185,8 @@ __global__ __launch_bounds__(BLOCK) void transport_kernel(DevGrid G, DevRun R) {
                     const int cell = cr + G.nr * (ct + G.ntheta * cp);
                     const int m = G.matid[cell];
                     double alpha, beta;
-                    sample_angles(G, R, G.cums + (size_t)m * CUM_DOUBLES, rng, st, alpha, beta);
+                    double c2b_unused, s2b_unused;
+                    sample_angles(G, R, G.cums + (size_t)m * CUM_DOUBLES, rng, st, alpha, beta, c2b_unused, s2b_unused);
                     double e0, e1, e2;
                     direction_cosine(R, alpha, beta, dx, dy, dz, e0, e1, e2);
                     double sc[16];
