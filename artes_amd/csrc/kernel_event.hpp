@@ -315,9 +315,11 @@ struct WaveQueue {
     }
 };
 
-// park the packet in a new propagation trace starting at its position
+// park the packet in a new propagation trace starting at its position (an interaction
+// point: no face; the field carried the matrix id, see event_one)
 __device__ __forceinline__ void start_prop(const Pool& S, int slot, double tau) {
     S.s[slot].ttgt = tau;
+    S.s[slot].pface = 0;
     S.s[slot].mode = S_PROP;
 }
 
@@ -494,10 +496,9 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         // 674-676, 801-807); the polarised components follow by the same factor
         const double wI = L0.wI;
         double st[4] = {wI, L0.q1 * wI, L0.q2 * wI, L0.q3 * wI};
-        int cr, ct, cp;
-        unpack_cell(L0.pcell, cr, ct, cp);
-        const int cell = cr + G.nr * (ct + G.ntheta * cp);
-        const int mid = G.nmat == 1 ? 0 : G.matid[cell];   // uniform atmosphere: no dependent load
+        // the interaction cell's matrix id, left in the face field by k_trace's interaction
+        // block (an interaction point lies on no face; reset below when the next trace starts)
+        const int mid = G.nmat == 1 ? 0 : L0.pface;
         using TL = TabLayout<PAD>;     // the matrices
         using TC = TabLayout<PADC>;    // the cumulative sampling tables
         const double* __restrict__ P = G.mats + (size_t)mid * TL::MAT;

@@ -626,7 +626,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         }
 #endif
         pcell = pack_cell(tcr, tct, tcp);
-        pface = 0;
+        // an interaction point lies on no face; until k_event starts the next trace the face
+        // field carries the cell's scattering-matrix id instead, so k_event needs no dependent
+        // read of the per-cell id table (k_event resets it to 0).  The load's result is only
+        // stored at the chain's end.
+        pface = G.nmat > 1 ? G.matid[cell] : 0;
         if (kb) {   // a backward trace: count the steps the forward one takes
             c_cross += (uint32_t)(kb - 2 * ncross);
             ncross = kb - ncross;
@@ -777,19 +781,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 e0 = dm;
                 sides = (outer ? 1 : 0) | ((retry ? 1 : 0) << 4);
             }
-            // the evaluated family's entry is exact now: clear ITS bit.  (The round-2 "nearest
-            // bound first" variant evaluated a family other than the lowest pending one but kept
-            // `pending &= pending - 1`, which clears the LOWEST bit: that family's bound was then
-            // taken for an exact distance, the lane stepped onto it as onto a face, and next_cell
-            // walked the cell indices out of range -- the illegal access of that round, DESIGN.md
-            // §4; ARTES_DEBUG counts such a clear as ARTES_ERR_PENDING.)
+            // the evaluated family's entry is exact now: clear ITS bit (fam is always a pending
+            // family, so the xor clears it; two instructions, as `pending & (pending - 1)`).
+            // (The round-2 "nearest bound first" variant evaluated a family other than the lowest
+            // pending one but kept `pending &= pending - 1`, which clears the LOWEST bit: that
+            // family's bound was then taken for an exact distance, the lane stepped onto it as
+            // onto a face, and next_cell walked the cell indices out of range -- the illegal
+            // access of that round; ARTES_DEBUG counts such a clear as
+            // ARTES_ERR_PENDING.)
 #ifdef ARTES_DEBUG
             const int pending_before = pending;
 #endif
 #ifdef ARTES_OLD_CLEAR
             if (!retry) pending &= pending - 1;   // (development build: the round-2 clear)
 #else
-            if (!retry) pending &= ~(1 << fam);
+            if (!retry) pending ^= 1 << fam;
 #endif
 #ifdef ARTES_DEBUG
             if (!retry && (pending_before & ~pending) != (1 << fam)) log_err(R, ARTES_ERR_PENDING);
