@@ -162,3 +162,58 @@ def test_cloudy_cli_gpu_matches_oracle_cli(require_gpu, cloudy, mode, out):
     if mode == "spectrum":   # optical_depth.dat (ARTES.f90:2457-2491): the same file from both runs
         od = (root / f"output/g_{mode}/output/optical_depth.dat").read_text()
         assert od == (root / f"output/o_{mode}/output/optical_depth.dat").read_text() and len(od.splitlines()) == 5
+
+
+# ------------------------------------------------------------------------------------------
+# configs[3] at its stated wavelength count: the same gas + Mie-cloud atmosphere over 50
+# wavelengths 0.45-0.95 micron (401 distinct matrices; the k_event LDS_C path, the call's
+# wavelength's ~9 matrices renumbered per call).  Trajectories at 8 of the 50 wavelengths and
+# the full 50-wavelength spectrum through the CLI, GPU against oracle.
+
+@pytest.fixture(scope="module")
+def cloudy50(tmp_path_factory):
+    root = tmp_path_factory.mktemp("cloudy50")
+    d = root / "input" / "cloudy50"
+    wl = tuple(np.round(np.linspace(0.45, 0.95, 50), 6))
+    atm = synthetic.make_cloudy(str(d), wavelength=wl)
+    return root, d, atm
+
+
+@pytest.mark.parametrize("wl", [0, 7, 14, 21, 28, 35, 42, 49])
+def test_cloudy50_trajectories_match_oracle(require_gpu, oracle_mod, cloudy50, wl):
+    from artes_amd.engine import Grid
+
+    _, _, atm = cloudy50
+    grid = Grid(atm, device=0)
+    assert grid.num_matrices() > 300
+    og = oracle_mod.OracleGrid(atm)
+    cfg = driver.default_config()
+    cfg.apply("detector:type", "phase")
+    det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
+    p = driver.run_params(cfg, det, wl, det_phi=math.radians(2.5 * wl), cell_depth=og.cell_depth(wl))
+    n = 20000
+    gpu = grid.trace(p, 0, n, 4242 + wl)
+    ref = og.run(p, 0, n, 4242 + wl, records=True)[4]
+    grid.close()
+    same = _same(gpu, ref)
+    short = ref[:, 1] <= 20
+    assert same[short].mean() >= 0.999 and same.mean() >= 0.99, (wl, same.mean(), same[short].mean())
+    assert gpu[:, 1].mean() > 1.0 and gpu[:, 0].sum() > 0
+
+
+def test_cloudy50_spectrum_cli_gpu_matches_oracle_cli(require_gpu, cloudy50):
+    from test_cli import OracleTransport
+
+    root, d, _ = cloudy50
+    (d / "artes.in").write_text(ARTES_IN.format(mode="spectrum"))
+    assert runner.run(["cloudy50", "3000", "-o", "g50", "--seed", "12"], root=str(root)) == 0
+    assert runner.run(["cloudy50", "3000", "-o", "o50", "--seed", "12"], root=str(root),
+                      transport_factory=OracleTransport) == 0
+    for f in ("spectrum.dat", "optical_depth.dat", "normalization.dat", "cell_depth.dat"):
+        g = _rows(root / f"output/g50/output/{f}")
+        o = _rows(root / f"output/o50/output/{f}")
+        assert g.shape == o.shape and g.shape[0] == 50, f
+        np.testing.assert_allclose(g[:, 0], o[:, 0], rtol=1e-12)
+        scale = np.abs(o[:, 1:]).max(axis=0)
+        assert np.all(np.abs(g[:, 1:] - o[:, 1:]) <= 1e-3 * scale + 1e-3 * np.abs(o[:, 1:])), f
+    assert (root / "output/g50/error.log").read_text() == (root / "output/o50/error.log").read_text()
