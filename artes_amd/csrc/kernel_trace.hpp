@@ -477,13 +477,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     // side (bit f of `sides`: 0 inner, 1 outer face)
     double e0 = INF, e1 = INF, e2 = INF;
     int sides = 0;
+    // crossings: counted per packet (ncross, in the record) and added to the lane's total
+    // once per chain, from the chain's start value nc0 (not per step)
     uint32_t c_cross = 0, c_peel = 0;
+    int nc0 = 0;
     // backward propagation after the forced first interaction (see the FIRST-trace end).
     // During a first trace: the packet's crossings when it started.  During the backward
     // trace that may follow: 2 x crossings at its start + the first trace's steps + 1
     // (from which the forward walk's step count follows at the interaction).  0 otherwise.
     int kb = 0;
-    int tsteps = 0;   // steps of the current trace (runaway guard)
+    int nlim = 0;   // the packet's crossing count at which the current trace is a runaway
     int parked = 0;   // 1: waiting for the batched forced first interaction (3: after a cell error)
 
     // Lazy set-up (3D grids, one-face evaluation).  A new trace needs every family's
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         Axy = dir_axy(ax2, by2, nx, ny);
         Az = cz2 * nz * nz;
         tacc = 0.0;
-        tsteps = 0;
+        nlim = ncross + (1 << 22);
         pending = fam_all;
         sides = 0;
         set_bounds();
@@ -549,7 +552,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             nx = R.det0; ny = R.det1; nz = R.det2;
             Axy = det_Axy; Az = det_Az; inz = det_inz;
             tacc = 0.0;
-            tsteps = 0;
+            nlim = ncross + (1 << 22);
             pending = fam_all;
             sides = 0;
             set_bounds();
@@ -619,8 +622,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             const double S2 = ax2 * px * px + by2 * py * py + cz2 * pz * pz;
             if (S2 < G.rf2[tcr] * (1 - 1e-9) || S2 > G.rf2[tcr + 1] * (1 + 1e-9)) {
                 if (atomicAdd(&R.err[ARTES_ERR_GEOM], 1ULL) < 6)
-                    printf("[geom] hit outside shell: t %.17g %.17g %.17g n %.17g %.17g %.17g cell %d %d %d face %d %d e %.17g %.17g %.17g sides %x s %.17g tsteps %d mode %d S2/rf2 %.17g %.17g\n",
-                           tx, ty, tz, nx, ny, nz, tcr, tct, tcp, tft, tfi, e0, e1, e2, sides, s, tsteps, mode,
+                    printf("[geom] hit outside shell: t %.17g %.17g %.17g n %.17g %.17g %.17g cell %d %d %d face %d %d e %.17g %.17g %.17g sides %x s %.17g steps left %d mode %d S2/rf2 %.17g %.17g\n",
+                           tx, ty, tz, nx, ny, nz, tcr, tct, tcp, tft, tfi, e0, e1, e2, sides, s, nlim - ncross, mode,
                            S2 / G.rf2[tcr], S2 / G.rf2[tcr + 1]);
             }
         }
@@ -632,7 +635,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         // stored at the chain's end.
         pface = G.nmat > 1 ? G.matid[cell] : 0;
         if (kb) {   // a backward trace: count the steps the forward one takes
-            c_cross += (uint32_t)(kb - 2 * ncross);
             ncross = kb - ncross;
             kb = 0;
         }
@@ -723,6 +725,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     rng.s0 = rec->r0; rng.s1 = rec->r1;
                     pcell = rec->pcell; pface = rec->pface;
                     ncross = rec->ncross;
+                    nc0 = ncross;
                     wI = rec->wI;
                     const bool peel = is_peel_trace(mode);
                     start_trace(peel ? R.det0 : ldx, peel ? R.det1 : ldy, peel ? R.det2 : ldz);
@@ -850,7 +853,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 // a trace of 2^22 steps is a schedule or geometry bug, not a history (~100
                 // crossings per packet, a few thousand at most): drop the packet with error
                 // ARTES_ERR_RUNAWAY instead of spinning
-                const bool runaway = ++tsteps > (1 << 22);
+                const bool runaway = ncross >= nlim;
                 const bool err31 = !(best < K.inf) | runaway;
                 const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
                 const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
@@ -870,7 +873,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     if (runaway) log_err(R, ARTES_ERR_RUNAWAY);
                     log_err(R, err31 ? 31 : 34);
                 }
-                c_cross++;
                 ncross++;
                 const double tau_cell = best * k;
                 const bool prop = (mode == S_PROP);
@@ -949,6 +951,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             }   // pending == 0
         }   // have
         if (end) {   // write the packet state back once
+            c_cross += (uint32_t)(ncross - nc0);
             Slot* rec = S.s + slot;
             rec->px = px; rec->py = py; rec->pz = pz;
             rec->r0 = rng.s0; rec->r1 = rng.s1;

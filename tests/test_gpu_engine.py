@@ -84,6 +84,17 @@ def test_backward_propagation_matches_forward(require_gpu, name, spec):
     assert c_back == pytest.approx(c_fwd, rel=1e-3)
 
 
+@pytest.mark.parametrize("name,spec", [("hg", {}), ("ray3d", dict(nr=10, ntheta=6, nphi=8, tau=3.0))])
+def test_crossing_counter_is_sum_of_packet_crossings(require_gpu, name, spec):
+    """k_trace adds a packet's crossings to the run's counter once per chain of traces
+    (kernel_trace.hpp, the chain-end write-back), backward walks counted as the forward
+    one: the counter of a run is the sum of the per-packet crossings its records report."""
+    atm, grid, p = _setup(name, **spec)
+    rec = grid.trace(p, 0, 50000, 12)
+    c = grid.run(p, 0, 50000, 12).counter("crossings")
+    assert c == pytest.approx(rec[:, 2].sum(), rel=1e-4)
+
+
 def test_packet_moments_are_pure_diagnostics(require_gpu):
     """packet_moments = 0 (the CLI / bench setting) transports the same packets: every
     detector plane the reference writes, the counters and the fluxes are identical; only
