@@ -51,6 +51,7 @@ struct DevGrid {
 struct DevRun {
     uint64_t first, n, seed;
     int nx, ny, photon_scattering, phase_far, stellar_direction, defer, refill, static_q64, batch, batch_min, hbatch;
+    int late_append;                // k_trace: list appends of ended chains at the wave's next refill (kernel_trace.hpp)
     int photon_source, photon_emission;
     int moments;                    // accumulate packet-level moments (slot line 1, planes 12-15, tot2[0..3])
     int emit_first;                 // trace-list order (kernel_event.hpp, Lists)
@@ -59,7 +60,6 @@ struct DevRun {
     double det0, det1, det2, sdt, cdt, sdp, cdp;
     double det_phi;                 // atan2(det1, det0) in [0, 2 pi] (peel_photon, ARTES.f90:4868-4870)
     double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
-    double omfstop;                 // 1 - fstop (the albedo weight's divisor, ARTES.f90:804)
     double* __restrict__ det;       // [NCOPY][4][4][ny][nx]
     size_t det_stride;              // doubles per copy
     double* __restrict__ tot2;      // [6] packet-level sum T^2 per Stokes, flux_emitted, flux_exit

@@ -287,10 +287,12 @@ __device__ __forceinline__ void wave_append(bool want, int val, int* list, int* 
     if (want) list[base + __popcll(mask & ((1ULL << lane) - 1ULL))] = val;
 }
 
-// Per-wave LDS staging queue (64 entries) in front of a global list, for producers whose
-// lanes finish at scattered times (k_trace): flushed with one atomic per 64 entries.
+// Per-wave LDS staging queue in front of a global list, for producers whose lanes finish at
+// scattered times (k_trace): 128 entries, flushed with one atomic once 64 or more wait
+// (`flush_if`, called where the atomic's round trip is off the critical path: a push of up
+// to 64 entries never has to flush first).
 struct WaveQueue {
-    int* buf;     // this wave's 64 LDS entries
+    int* buf;     // this wave's 128 LDS entries
     int cnt;      // wave-uniform fill level
     __device__ __forceinline__ void flush(int* list, int* list_n) {
         if (cnt == 0) return;
@@ -300,14 +302,17 @@ struct WaveQueue {
         base = __shfl(base, 0);
         __builtin_amdgcn_wave_barrier();
         if (lane < cnt) list[base + lane] = buf[lane];
+        if (lane + 64 < cnt) list[base + lane + 64] = buf[lane + 64];
         __builtin_amdgcn_wave_barrier();
         cnt = 0;
     }
-    __device__ __forceinline__ void push(bool want, int val, int* list, int* list_n) {
+    __device__ __forceinline__ void flush_if(int at, int* list, int* list_n) {
+        if (cnt >= at) flush(list, list_n);
+    }
+    __device__ __forceinline__ void push(bool want, int val) {
         const unsigned long long mask = __ballot(want);
         const int k = __popcll(mask);
         if (k == 0) return;
-        if (cnt + k > 64) flush(list, list_n);
         const int lane = threadIdx.x & 63;
         if (want) buf[cnt + __popcll(mask & ((1ULL << lane) - 1ULL))] = val;
         __builtin_amdgcn_wave_barrier();

@@ -426,8 +426,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     const int n = *L.trace_in_n;
     const int split = *L.trace_in_split;   // [0, split): new packets' traces; then k_event's, stored backwards
     const int home = sub_block() & 7;
-    __shared__ int s_q[2][BLOCK];
-    const int wbase = threadIdx.x & ~63;
+    __shared__ int s_q[2][2 * BLOCK];
+    const int wbase = 2 * (threadIdx.x & ~63);
     WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
     // the wave's trace-list cursor lives in LDS between refills (a wave refills every ~10
     // iterations; kept in registers it occupied scalar registers that the step's lane masks
@@ -458,10 +458,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     Rng rng{0, 0};
     int tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0, pending = 0, cell = 0;
     double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, inz = 0, Axy = 0, Az = 0;
-    // extinction and albedo of the current cell, loaded when the cell changes: the L2 round
+    // extinction and albedo weight of the current cell, loaded when the cell changes: the L2 round
     // trip overlaps the next iteration's face evaluation (one 16-byte load at a 32-bit byte
     // offset; ncell < 2^28, checked at grid creation)
-    double kext = 0, alb = 0;
+    double kext = 0, gam = 0;
     auto load_cell = [&]() {
 #ifdef ARTES_DEBUG
         if ((unsigned)cell >= (unsigned)G.ncell) {   // (ARTES_ERR_CELL: no out-of-range table read)
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #endif
         const double2 kv = *(const double2*)((const char*)G.ka + ((unsigned)cell << 4));
         kext = kv.x;
-        alb = kv.y;
+        gam = kv.y;
     };
     // per family (radial, theta, phi) the distance to the nearest face ahead, and its
     // side (bit f of `sides`: 0 inner, 1 outer face)
@@ -488,6 +488,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     int kb = 0;
     int nlim = 0;   // the packet's crossing count at which the current trace is a runaway
     int parked = 0;   // 1: waiting for the batched forced first interaction (3: after a cell error)
+    int pend = 0;     // the end mode of a chain whose list append waits for the wave's next refill
 
     // Lazy set-up (3D grids, one-face evaluation).  A new trace needs every family's
     // distance before its first step, one family per iteration, so two of every trace's
@@ -641,17 +642,30 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         if constexpr (FLOW) flow_segment(R.flow_g, R.flow_t, cell, px, py, pz, nx, ny, nz, s, wI, -1);   // (715, 874)
         const double xi = rng.uni();   // a killed packet's RNG state is not used again
         bool kill = !R.photon_scattering || xi < R.fstop;
-        if (alb < 1.0 && alb > 0.0) wI *= alb / R.omfstop;
+        wI *= gam;   // albedo / (1 - fstop) where 0 < albedo < 1, else 1 (ARTES.f90:801-805; the table, transport.hip)
+        __builtin_amdgcn_sched_barrier(0);   // (a scheduling boundary, as the old branch was: 5 registers fewer)
         kill = kill || wI <= R.pmin;
         if (kill) return S_END_ABS;
         // peel-off trace (ARTES.f90:4722-4761) from the interaction point: same cell (kext,
-        // alb stay), no face
+        // gam stay), no face
         c_peel++;
         mode = S_PEEL;
         tx = px; ty = py; tz = pz;
         tft = 0; tfi = 0;
         set_direction_det();
         return 0;
+    };
+
+    // A chain that ends writes its record back at once; its slot is appended to the event or
+    // emit list by `append` (call with the whole wave: the appends are wave-aggregated) at
+    // the end of the iteration, or with R.late_append at the wave's next refill (and after the
+    // loop): one append block for the ~16 lanes of a refill instead of two in every iteration.
+    // (Deferring the record stores too kept the ended packets' state live across iterations:
+    // 16 spilled registers.)
+    auto append = [&]() {
+        q_event.push(pend && to_event_list(pend), slot);
+        q_emit.push(pend && !to_event_list(pend), emit_entry(slot, pend));
+        pend = 0;
     };
 
     // watchdog: a wave runs ~1e4 iterations per launch at the largest pool; a schedule bug
@@ -697,6 +711,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         if (!exhausted) {
             const unsigned long long idle = __ballot(!have);
             if (__popcll(idle) >= R.refill || idle == __ballot(true)) {
+                append();
                 TraceCursor cur = load_cursor(my_cur);
                 const int my = wave_take(cur, L.grab, home, !have);
                 if ((threadIdx.x & 63) == 0) *my_cur = cur;
@@ -950,7 +965,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }   // pending == 0
         }   // have
-        if (end) {   // write the packet state back once
+        if (end) {   // the chain ends: the record now, the list append below or at the next refill
             c_cross += (uint32_t)(ncross - nc0);
             Slot* rec = S.s + slot;
             rec->px = px; rec->py = py; rec->pz = pz;
@@ -960,8 +975,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             rec->wI = wI;
             rec->tpeel = tacc;
             rec->ttgt = ttgt;
+            pend = end;
             have = false;
         }
+        if (!R.late_append) append();
+        q_event.flush_if(64, L.event, L.event_n);
+        q_emit.flush_if(64, L.emit, L.emit_n);
 #ifdef ARTES_DEBUG_LANES
         {
             const unsigned long long bs = __ballot(dbg_s), bh = __ballot(dbg_h), bm = __ballot(dbg_m);
@@ -969,9 +988,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             dbg_nretry += __popcll(__ballot(dbg_r)); dbg_nsetup += __popcll(__ballot(dbg_u));
         }
 #endif
-        q_event.push(end && to_event_list(end), slot, L.event, L.event_n);
-        q_emit.push(end && !to_event_list(end), emit_entry(slot, end), L.emit, L.emit_n);
     }
+    append();
     q_event.flush(L.event, L.event_n);
     q_emit.flush(L.emit, L.emit_n);
 #ifdef ARTES_DEBUG_LANES

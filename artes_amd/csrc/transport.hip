@@ -72,6 +72,7 @@ struct artes_grid {
     double *d_rf2 = nullptr, *d_thetaf = nullptr, *d_tan2 = nullptr, *d_phif = nullptr, *d_phis = nullptr,
            *d_phic = nullptr, *d_kappa = nullptr, *d_albedo = nullptr, *d_ka = nullptr, *d_mats = nullptr, *d_cums = nullptr,
            *d_sc2 = nullptr, *d_ss2 = nullptr;
+    double ka_fstop = -1.0;   // the fstop d_ka's gamma column was built for (launch); -1: not yet
     int *d_tplane = nullptr, *d_matid = nullptr;
     double *d_rfront = nullptr, *d_tcos = nullptr;
     double *d_th_cdf = nullptr, *d_th_weight = nullptr;   // thermal tables of the last planet-source call
@@ -238,11 +239,7 @@ int32_t artes_grid_create(const artes_grid_desc* desc, int32_t device, artes_gri
     HIP_TRY(upload(&g->d_phic, T.phic));
     HIP_TRY(upload(&g->d_kappa, T.kappa));
     HIP_TRY(upload(&g->d_albedo, T.albedo));
-    {
-        std::vector<double> ka(2 * T.kappa.size());
-        for (size_t i = 0; i < T.kappa.size(); i++) { ka[2 * i] = T.kappa[i]; ka[2 * i + 1] = T.albedo[i]; }
-        HIP_TRY(upload(&g->d_ka, ka));
-    }
+    HIP_TRY(hipMalloc((void**)&g->d_ka, 2 * T.kappa.size() * sizeof(double)));   // (filled by launch: ka_table)
     HIP_TRY(upload(&g->d_sc2, T.sc2));
     HIP_TRY(upload(&g->d_ss2, T.ss2));
     HIP_TRY(upload(&g->d_rfront, T.rfront));
@@ -660,6 +657,24 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     G.phif = g->d_phif; G.phis = g->d_phis; G.phic = g->d_phic;
     G.kappa = g->d_kappa + (size_t)p->wl_index * T.ncell;
     G.albedo = g->d_albedo + (size_t)p->wl_index * T.ncell;
+    // k_trace's per-cell table: (kappa, gamma), gamma the scattering-loop head's weight
+    // albedo / (1 - fstop) where 0 < albedo < 1, else 1 (ARTES.f90:801-805) -- the reference's
+    // division, done once per cell on the host instead of per interaction on the device
+    // (a multiply by 1 where the reference skips it: the same weight bit for bit); rebuilt
+    // when a call brings another fstop
+    if (g->ka_fstop != p->fstop) {
+        std::vector<double> ka(2 * T.kappa.size());
+        const double om = 1.0 - p->fstop;
+        for (size_t i = 0; i < T.kappa.size(); i++) {
+            const double a = T.albedo[i];
+            ka[2 * i] = T.kappa[i];
+            ka[2 * i + 1] = (a < 1.0 && a > 0.0) ? a / om : 1.0;
+        }
+        HIP_TRY(hipStreamSynchronize(stream));   // (no earlier call on this stream still reads the old table)
+        HIP_TRY(hipMemcpyAsync(g->d_ka, ka.data(), ka.size() * sizeof(double), hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipStreamSynchronize(stream));   // (the host vector goes out of scope)
+        g->ka_fstop = p->fstop;
+    }
     G.ka = g->d_ka + 2 * (size_t)p->wl_index * T.ncell;
     {
         artes_grid::WlSet* W = nullptr;
@@ -684,6 +699,11 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // (coarse 3D grids -- the cloudy atmospheres of configs[3], ~600 cells -- have short traces
     // and refill best at 32: cloudy phase +2.7 %, spectrum +4 %, profiles/r03/cloudy_ldsc_refill.txt)
     R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? (T.ncell < 4096 ? 32 : 16) : 20);
+    // ended chains' list appends at the wave's next refill (kernel_trace.hpp `append`): ray3d
+    // +3.7 %, hg +5.1 %, iso +2.7 %, the cloudy configs[3] calls +3.4-3.8 % (3e8 / 1e8 packets,
+    // profiles/r03/late_append_ab.txt)
+    const char* la = getenv("ARTES_LATE_APPEND");
+    R.late_append = la ? (atoi(la) != 0) : 1;
     const char* ef = getenv("ARTES_EMIT_FIRST");
     R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
     const char* bw = getenv("ARTES_BACKWARD");
@@ -713,7 +733,6 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     if (R.det_phi < 0.0) R.det_phi += 2.0 * M_PI;
     if (R.det_phi > 2.0 * M_PI) R.det_phi -= 2.0 * M_PI;
     R.x_max = p->x_max; R.y_max = p->y_max; R.fstop = p->fstop; R.pmin = p->photon_minimum;
-    R.omfstop = 1.0 - p->fstop;
     R.surface_albedo = p->surface_albedo; R.theta_star = p->theta_star; R.phi_star = p->phi_star;
     R.det = g->d_copies; R.det_stride = stride;
     R.tot2 = tot_out; R.cnt = cnt_out; R.err = err_out; R.rec = rec;
@@ -893,12 +912,17 @@ int32_t artes_kernel_times(artes_grid* g, double* ms, uint64_t* launches) {
     if (g->prof_used == 0) return 0;
     HIP_TRY(hipSetDevice(g->device));
     HIP_TRY(hipEventSynchronize(g->prof_ev[2 * g->prof_used - 1]));
+    // (development: ARTES_LAUNCH_LOG=<file> appends every launch's kind and time, one line per call)
+    const char* log = getenv("ARTES_LAUNCH_LOG");
+    FILE* lf = log ? fopen(log, "a") : nullptr;
     for (size_t i = 0; i < g->prof_used; i++) {
         float t = 0.0f;
         HIP_TRY(hipEventElapsedTime(&t, g->prof_ev[2 * i], g->prof_ev[2 * i + 1]));
         ms[g->prof_kind[i]] += (double)t;
         if (launches) launches[g->prof_kind[i]] += 1;
+        if (lf) fprintf(lf, "%d:%.4f ", g->prof_kind[i], t);
     }
+    if (lf) { fprintf(lf, "\n"); fclose(lf); }
     g->prof_used = 0;
     return 0;
 }

@@ -9,7 +9,12 @@ from artes_amd.engine import Grid  # noqa: E402
 name = sys.argv[1] if len(sys.argv) > 1 else "ray3d"
 n = int(float(sys.argv[2])) if len(sys.argv) > 2 else 10**7
 cfg = driver.default_config()
-atm = synthetic.make_config(name, share_matrix=True)
+if name == "cloudy":   # configs[3]'s shape (gas + Mie cloud, 16x6x6), a phase-curve call at 0.45 um
+    import tempfile
+    atm = synthetic.make_cloudy(tempfile.mkdtemp(), wavelength=(0.45, 0.7))
+    cfg.apply("detector:type", "phase")
+else:
+    atm = synthetic.make_config(name, share_matrix=True)
 det = driver.detector_geometry(cfg, atm["radial"][-1])
 g = Grid(atm, 0)
 p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0), packet_moments=False)
