@@ -322,8 +322,18 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
                 log_err(R, 12);
             }
         }
-        if (beta >= 0.0 && beta < PI) mueller(beta2, c, s);
-        else if (beta >= PI && beta < TWO_PI) mueller(-beta2, c, s);
+        // mueller(beta2) or mueller(-beta2) (ARTES.f90:1905-1910): the same cosine bit for bit
+        // (sincos_bounded is odd/even exactly), so one evaluation, no divergent pair; the sign
+        // of the sine by mueller_matrix_filler's quadrant rule for +beta2 or -beta2 (beta2 in
+        // [0, pi]: negative on (pi/2, pi) for +beta2, on (0, pi/2) for -beta2)
+        const bool rot_lo = beta >= 0.0 && beta < PI, rot_hi = beta >= PI && beta < TWO_PI;
+        if (rot_lo || rot_hi) {
+            const double c2 = cos_b(2.0 * beta2);
+            const double s2 = dsqrt(1.0 - c2 * c2);
+            const bool neg = rot_lo ? (beta2 > HALF_PI && beta2 < PI) : (beta2 > 0.0 && beta2 < HALF_PI);
+            c = c2;
+            s = neg ? -s2 : s2;
+        }
         so[0] = q[0];
         so[1] = c * q[1] + s * q[2];
         so[2] = -s * q[1] + c * q[2];
@@ -373,16 +383,18 @@ __device__ void direction_cosine(const DevRun& R, double alpha, double beta, dou
     double ctn = 0.0, phi_new = 0.0, spn = 0.0;
     const bool upper = (beta >= PI && beta < TWO_PI);
     const bool lower = (beta >= 0.0 && beta < PI);
-    if (upper) ctn = cto * alpha + sto * dsqrt(1.0 - alpha * alpha) * cos_b(TWO_PI - beta);
-    else if (lower) ctn = cto * alpha + sto * dsqrt(1.0 - alpha * alpha) * cos_b(beta);
+    // (one cosine of the branch's argument: the same value, no divergent pair)
+    const double cbeta = cos_b(upper ? TWO_PI - beta : beta);
+    if (upper || lower) ctn = cto * alpha + sto * dsqrt(1.0 - alpha * alpha) * cbeta;
     else log_err(R, 18);
     const double stn = dsqrt(1.0 - ctn * ctn);
     double num = (alpha - ctn * cto) / (stn * sto);
     if (num >= 1.0) num = 1.0 - 1.e-10;
     else if (num <= -1.0) num = -1.0 + 1.e-10;
     if (fabs(num) <= 1.0) {
-        if (upper) phi_new = phi_old - acos(num);
-        else if (lower) phi_new = phi_old + acos(num);
+        const double an = acos(num);
+        if (upper) phi_new = phi_old - an;
+        else if (lower) phi_new = phi_old + an;
         else log_err(R, 19);
     } else {
         log_err(R, 20);
