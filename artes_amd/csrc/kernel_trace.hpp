@@ -562,7 +562,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         }
     };
     // a trace starts at the packet position with zero optical depth
-    auto start_trace = [&](double d0, double d1, double d2) {
+    auto start_position = [&]() {
         tx = px; ty = py; tz = pz;
         unpack_cell(pcell, tcr, tct, tcp);
         unpack_face(pface, tft, tfi);
@@ -574,6 +574,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #endif
         cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
         load_cell();
+    };
+    auto start_trace = [&](double d0, double d1, double d2) {
+        start_position();
         set_direction(d0, d1, d2);
     };
 
@@ -600,13 +603,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         bool back = false;
         if constexpr (!FLOW) back = R.backward && mid && !err && tau_first - tau < tau;
         kb = back ? 2 * ncross + (ncross - kb) + 1 : 0;
+        // (one set_direction for both walks, on selected operands: the two inlined copies ran
+        // as a divergent pair, ~65 VALU instructions more per block)
         if (back) {
             ttgt = fmax(tau_first - tau, 0.0);   // tau rounds to <= tau_first + 1 ulp
-            set_direction(-nx, -ny, -nz);
         } else {
             ttgt = tau;
-            start_trace(nx, ny, nz);
+            start_position();
         }
+        const double sgn = back ? -1.0 : 1.0;
+        set_direction(sgn * nx, sgn * ny, sgn * nz);
     };
 
     // The interaction at the end of a propagation (ARTES.f90:705-720), then the
