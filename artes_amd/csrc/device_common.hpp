@@ -20,6 +20,7 @@ constexpr double TWO_PI = 2.0 * PI;
 // -------------------------------------------------------------- device data ---
 struct DevGrid {
     int nr, ntheta, nphi, ncell, nmat;
+    int msym;                            // mats holds the block-diagonal symmetric form (interp_matrix)
     int cell_depth;
     double ax2, by2, cz2, a, b;
     double rtop;
@@ -32,9 +33,9 @@ struct DevGrid {
     const double* __restrict__ phic;     // [nphi]
     const double* __restrict__ kappa;    // [ncell] (this wavelength)
     const double* __restrict__ albedo;   // [ncell]
-    const double* __restrict__ ka;       // [ncell][2]: extinction, albedo (k_trace: one 16-byte load per step)
+    const double* __restrict__ ka;       // [ncell][2]: extinction, albedo weight (k_trace: one 16-byte load per step)
     const int* __restrict__ matid;       // [ncell]
-    const double* __restrict__ mats;     // [nmat][180][16]
+    const double* __restrict__ mats;     // [nmat][180][16], or with msym [nmat][180][4] = (P11, P12, P33, P34)
     const double* __restrict__ cums;     // [nmat][181][4]
     const double* __restrict__ sc2;      // [181]
     const double* __restrict__ ss2;      // [181]
@@ -412,14 +413,41 @@ __device__ void direction_cosine(const DevRun& R, double alpha, double beta, dou
 
 // linear interpolation of the 16 elements at angle acos(mu) between bin centres
 // (ARTES.f90:1448-1530, 4780-4862); P = [180][RS] of the cell's matrix (RS = 16, or 17
-// in LDS: see k_event)
-template <int RS = 16>
-__device__ __forceinline__ void interp_matrix(const double* __restrict__ P, double acos_mu, double sc[16]) {
+// in LDS: see k_event).  sym: the call's matrices all have the block-diagonal form of
+// spheres and Rayleigh scattering, [[P11 P12 0 0] [P12 P11 0 0] [0 0 P33 P34] [0 0 -P34 P33]]
+// (checked value by value on the host, wl_set), and P = [180][RS4] holds (P11, P12, P33, P34):
+// 4 reads and 4 interpolations per row instead of 16, the same 16 values bit for bit
+// (the duplicated elements interpolate identically, the zeros to +0, and -P34's
+// interpolation is the exact negative of P34's).
+template <int RS = 16, int RS4 = 4>
+__device__ __forceinline__ void interp_matrix(const double* __restrict__ P, bool sym, double acos_mu, double sc[16]) {
     const double deg = acos_mu * 180.0 / PI;
     const int ideg = (int)deg;
     int up, lo;
     if (deg - (double)ideg > 0.5) { up = ideg + 2; lo = ideg + 1; }
     else { up = ideg + 1; lo = ideg; }
+    if (sym) {
+        double v[4];
+        if (up == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[i] = P[i];
+        } else if (lo == 180) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[i] = P[179 * RS4 + i];
+        } else {
+            const double* x0 = P + (lo - 1) * RS4;
+            const double* x1 = P + (up - 1) * RS4;
+            const double y0 = (double)lo - 0.5, y1 = (double)up - 0.5;
+            const double f = (deg - y0) / (y1 - y0);
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[i] = (x1[i] - x0[i]) * f + x0[i];
+        }
+        sc[0] = v[0]; sc[1] = v[1]; sc[2] = 0.0; sc[3] = 0.0;
+        sc[4] = v[1]; sc[5] = v[0]; sc[6] = 0.0; sc[7] = 0.0;
+        sc[8] = 0.0; sc[9] = 0.0; sc[10] = v[2]; sc[11] = v[3];
+        sc[12] = 0.0; sc[13] = 0.0; sc[14] = -v[3]; sc[15] = v[2];
+        return;
+    }
     if (up == 1) {
 #pragma unroll
         for (int i = 0; i < 16; i++) sc[i] = P[i];

@@ -477,6 +477,8 @@ template <bool PAD>
 struct TabLayout {
     static constexpr int RS = PAD ? 17 : 16;            // matrix row stride
     static constexpr int MAT = NANG * RS;               // doubles per matrix
+    static constexpr int RS4 = PAD ? 5 : 4;             // row stride of the symmetric form (DevGrid::msym)
+    static constexpr int MAT4 = NANG * RS4;
     static constexpr int CS = PAD ? 5 : 4;              // cumulative-table entry stride
     static constexpr int CUM = (NANG + 1) * CS;         // doubles per cumulative table
 };
@@ -506,7 +508,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         const int mid = G.nmat == 1 ? 0 : L0.pface;
         using TL = TabLayout<PAD>;     // the matrices
         using TC = TabLayout<PADC>;    // the cumulative sampling tables
-        const double* __restrict__ P = G.mats + (size_t)mid * TL::MAT;
+        const bool sym = G.msym != 0;
+        const double* __restrict__ P = G.mats + (size_t)mid * (sym ? TL::MAT4 : TL::MAT);
         const double tau_peel = L0.tpeel;
         // the incoming direction's azimuth: the peel-off's phi_old (ARTES.f90:4868-4870) and the
         // scattering's (direction_cosine, 1975-1977) -- one atan2 for both
@@ -518,7 +521,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             if (mu >= 1.0) mu = 1.0 - 1.e-10;
             else if (mu <= -1.0) mu = -1.0 + 1.e-10;
             double sc[16];
-            interp_matrix<TL::RS>(P, acos(mu), sc);
+            interp_matrix<TL::RS, TL::RS4>(P, sym, acos(mu), sc);
             const double phi_new = R.det_phi;   // the detector's azimuth, once per run
             bool have_out = false;
             double so[4] = {0, 0, 0, 0};
@@ -596,7 +599,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         double e0, e1, e2;
         direction_cosine<true>(R, alpha, beta, dx, dy, dz, e0, e1, e2, phi_old);
         double sc[16];
-        interp_matrix<TL::RS>(P, acos(alpha), sc);
+        interp_matrix<TL::RS, TL::RS4>(P, sym, acos(alpha), sc);
         if (fabs(alpha) < 1.0) {
             double sn[4];
             polarization_rotation<true>(R, alpha, beta, st, sc, dz, e2, sn, false, c2b, s2b);
@@ -619,8 +622,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
 
 // doubles of LDS holding the scattering tables of k_event: matrices, cumulative
 // sampling tables (padded, TabLayout<true>) and the azimuth tables
-__host__ __device__ inline size_t event_table_doubles(int nmat) {
-    return (size_t)nmat * (TabLayout<true>::MAT + TabLayout<true>::CUM) + 2 * (NANG + 1);
+__host__ __device__ inline size_t event_table_doubles(int nmat, bool sym) {
+    return (size_t)nmat * ((sym ? TabLayout<true>::MAT4 : TabLayout<true>::MAT) + TabLayout<true>::CUM) + 2 * (NANG + 1);
 }
 // the same for the cumulative tables and the azimuth tables alone (LDS_C)
 __host__ __device__ inline size_t event_cum_doubles(int nmat) {
@@ -668,12 +671,16 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
     }
     if constexpr (LDS_T) {
         using TL = TabLayout<true>;
-        const int nm = G0.nmat * MAT_DOUBLES, nc = G0.nmat * CUM_DOUBLES;
+        const int nc = G0.nmat * CUM_DOUBLES;
         double* m = s_ev;
-        double* c = m + G0.nmat * TL::MAT;
+        double* c = m + G0.nmat * (G0.msym ? TL::MAT4 : TL::MAT);
         double* a = c + G0.nmat * TL::CUM;
         double* b = a + (NANG + 1);
-        for (int i = threadIdx.x; i < nm; i += EB) m[(i >> 4) * TL::RS + (i & 15)] = G0.mats[i];   // rows of 16 -> 17
+        if (G0.msym) {
+            for (int i = threadIdx.x; i < G0.nmat * NANG * 4; i += EB) m[(i >> 2) * TL::RS4 + (i & 3)] = G0.mats[i];   // rows of 4 -> 5
+        } else {
+            for (int i = threadIdx.x; i < G0.nmat * MAT_DOUBLES; i += EB) m[(i >> 4) * TL::RS + (i & 15)] = G0.mats[i];   // rows of 16 -> 17
+        }
         for (int i = threadIdx.x; i < nc; i += EB) c[(i >> 2) * TL::CS + (i & 3)] = G0.cums[i];    // entries of 4 -> 5
         for (int i = threadIdx.x; i <= NANG; i += EB) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
         G.mats = m; G.cums = c; G.sc2 = a; G.ss2 = b;

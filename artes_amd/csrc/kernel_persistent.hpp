@@ -112,7 +112,7 @@ __global__ __launch_bounds__(BLOCK) void transport_kernel(DevGrid G, DevRun R) {
                     const int cell = cr + G.nr * (ct + G.ntheta * cp);
                     const double* __restrict__ P = G.mats + (size_t)G.matid[cell] * MAT_DOUBLES;
                     double sc[16];
-                    interp_matrix(P, acos(mu), sc);
+                    interp_matrix(P, false, acos(mu), sc);
                     double phi_old = atan2(dy, dx);
                     if (phi_old < 0.0) phi_old += TWO_PI;
                     if (phi_old > TWO_PI) phi_old -= TWO_PI;
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(BLOCK) void transport_kernel(DevGrid G, DevRun R) {
                     double e0, e1, e2;
                     direction_cosine(R, alpha, beta, dx, dy, dz, e0, e1, e2);
                     double sc[16];
-                    interp_matrix(G.mats + (size_t)m * MAT_DOUBLES, acos(alpha), sc);
+                    interp_matrix(G.mats + (size_t)m * MAT_DOUBLES, false, acos(alpha), sc);
                     if (fabs(alpha) < 1.0) {
                         double sn[4];
                         polarization_rotation(R, alpha, beta, st, sc, dz, e2, sn, false);

@@ -112,6 +112,7 @@ struct artes_grid {
     struct WlSet {
         int nmat = -1;
         double* d_mats = nullptr;   // [nmat][180][16]
+        double* d_mats4 = nullptr;  // [nmat][180][4] (P11, P12, P33, P34) when every matrix is block-diagonal symmetric
         double* d_cums = nullptr;   // [nmat][181][4]
         int* d_matid = nullptr;     // [ncell] local ids
     };
@@ -207,6 +208,7 @@ void artes_grid_destroy(artes_grid* g) {
         if (p) hipFree(p);
     for (auto& W : g->wl) {
         if (W.d_mats) hipFree(W.d_mats);
+        if (W.d_mats4) hipFree(W.d_mats4);
         if (W.d_cums) hipFree(W.d_cums);
         if (W.d_matid) hipFree(W.d_matid);
     }
@@ -307,6 +309,23 @@ static int32_t wl_set(artes_grid* g, int wl, artes_grid::WlSet** out) {
         }
         HIP_TRY(upload(&W.d_mats, mats));
         HIP_TRY(upload(&W.d_cums, cums));
+        // the block-diagonal form of spheres and Rayleigh scattering, value by value (interp_matrix):
+        // k_event then reads 4 of the 16 elements per row (ARTES_MSYM=0 turns it off)
+        bool sym = true;
+        for (size_t k = 0; k < mats.size() && sym; k += NELEM) {
+            const double* m = &mats[k];
+            sym = m[2] == 0.0 && m[3] == 0.0 && m[6] == 0.0 && m[7] == 0.0 && m[8] == 0.0 && m[9] == 0.0 && m[12] == 0.0 &&
+                  m[13] == 0.0 && m[4] == m[1] && m[5] == m[0] && m[15] == m[10] && m[14] == -m[11];
+        }
+        const char* ms = getenv("ARTES_MSYM");
+        if (sym && !(ms && atoi(ms) == 0)) {
+            std::vector<double> m4(ids.size() * NANG * 4);
+            for (size_t r = 0; r < ids.size() * NANG; r++) {
+                const double* m = &mats[r * NELEM];
+                m4[4 * r] = m[0]; m4[4 * r + 1] = m[1]; m4[4 * r + 2] = m[10]; m4[4 * r + 3] = m[11];
+            }
+            HIP_TRY(upload(&W.d_mats4, m4));
+        }
         HIP_TRY(upload(&W.d_matid, matid));
         W.nmat = (int)ids.size();
     }
@@ -448,7 +467,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     if (trace_table_bytes(G.nr, G.ntheta, G.nphi) > 65536) return fail(-22, "face tables exceed the 64 KiB LDS budget of k_trace");
     // scattering tables in LDS for k_event when they fit next to one another (a few
     // distinct matrices: uniform and layered atmospheres); otherwise read from L2
-    const size_t ev_bytes = event_table_doubles(G.nmat) * sizeof(double);
+    const size_t ev_bytes = event_table_doubles(G.nmat, G.msym != 0) * sizeof(double);
     const char* el = getenv("ARTES_EVENT_LDS");
     const bool ev_lds = (el ? atoi(el) != 0 : true) && ev_bytes <= 65536;
     // planes 0-8 of the detector accumulated per k_event block in LDS when they fit
@@ -680,7 +699,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
         artes_grid::WlSet* W = nullptr;
         const int32_t rc = wl_set(g, p->wl_index, &W);
         if (rc) return rc;
-        G.nmat = W->nmat; G.matid = W->d_matid; G.mats = W->d_mats; G.cums = W->d_cums;
+        G.nmat = W->nmat; G.matid = W->d_matid; G.cums = W->d_cums;
+        // (the persistent engine reads the 16-element form)
+        G.msym = (W->d_mats4 && use_event_engine()) ? 1 : 0;
+        G.mats = G.msym ? W->d_mats4 : W->d_mats;
     }
     G.sc2 = g->d_sc2; G.ss2 = g->d_ss2;
 
