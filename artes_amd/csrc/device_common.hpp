@@ -437,8 +437,7 @@ __device__ __forceinline__ void interp_matrix(const double* __restrict__ P, bool
         } else {
             const double* x0 = P + (lo - 1) * RS4;
             const double* x1 = P + (up - 1) * RS4;
-            const double y0 = (double)lo - 0.5, y1 = (double)up - 0.5;
-            const double f = (deg - y0) / (y1 - y0);
+            const double f = deg - ((double)lo - 0.5);   // (the reference divides by y1 - y0 = 1: exact)
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = (x1[i] - x0[i]) * f + x0[i];
         }
@@ -457,8 +456,7 @@ __device__ __forceinline__ void interp_matrix(const double* __restrict__ P, bool
     } else {
         const double* x0 = P + (lo - 1) * RS;
         const double* x1 = P + (up - 1) * RS;
-        const double y0 = (double)lo - 0.5, y1 = (double)up - 0.5;
-        const double f = (deg - y0) / (y1 - y0);
+        const double f = deg - ((double)lo - 0.5);   // (the reference divides by y1 - y0 = 1: exact)
 #pragma unroll
         for (int i = 0; i < 16; i++) sc[i] = (x1[i] - x0[i]) * f + x0[i];
     }
