@@ -288,11 +288,23 @@ __device__ __forceinline__ void wave_append(bool want, int val, int* list, int* 
 }
 
 // Per-wave LDS staging queue in front of a global list, for producers whose lanes finish at
-// scattered times (k_trace): 128 entries, flushed with one atomic once 64 or more wait
-// (`flush_if`, called where the atomic's round trip is off the critical path: a push of up
-// to 64 entries never has to flush first).
+// scattered times (k_trace): QCAP entries, flushed with one atomic once QFLUSH or more wait
+// (`flush_if`, called where the atomic's round trip is off the critical path: with
+// QFLUSH + 64 <= QCAP a push of up to 64 entries never has to flush first).  Every wave of a
+// sub-engine flushes into the same counter, and same-address atomics serialise at the
+// memory side: flushing every 192 entries instead of every 64 took iso's k_trace from 196.6
+// to 162.5 ms per 3e8 packets (hg -0.5 %, cloudy -1 %, ray3d the same); 512 and 1024
+// measured the same as 256 (profiles/r03/queue_size_ab.txt).
+#ifndef ARTES_QCAP
+#define ARTES_QCAP 256
+#endif
+#ifndef ARTES_QFLUSH
+#define ARTES_QFLUSH 192
+#endif
+constexpr int QCAP = ARTES_QCAP, QFLUSH = ARTES_QFLUSH;
+static_assert(QFLUSH + 64 <= QCAP, "a push of 64 entries fits without a flush");
 struct WaveQueue {
-    int* buf;     // this wave's 128 LDS entries
+    int* buf;     // this wave's QCAP LDS entries
     int cnt;      // wave-uniform fill level
     __device__ __forceinline__ void flush(int* list, int* list_n) {
         if (cnt == 0) return;
@@ -301,8 +313,7 @@ struct WaveQueue {
         if (lane == 0) base = atomicAdd(list_n, cnt);
         base = __shfl(base, 0);
         __builtin_amdgcn_wave_barrier();
-        if (lane < cnt) list[base + lane] = buf[lane];
-        if (lane + 64 < cnt) list[base + lane + 64] = buf[lane + 64];
+        for (int j = lane; j < cnt; j += 64) list[base + j] = buf[j];
         __builtin_amdgcn_wave_barrier();
         cnt = 0;
     }

@@ -426,8 +426,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     const int n = *L.trace_in_n;
     const int split = *L.trace_in_split;   // [0, split): new packets' traces; then k_event's, stored backwards
     const int home = sub_block() & 7;
-    __shared__ int s_q[2][2 * BLOCK];
-    const int wbase = 2 * (threadIdx.x & ~63);
+    __shared__ int s_q[2][QCAP * (BLOCK / 64)];
+    const int wbase = QCAP * (threadIdx.x >> 6);
     WaveQueue q_event{&s_q[0][wbase], 0}, q_emit{&s_q[1][wbase], 0};
     // the wave's trace-list cursor lives in LDS between refills (a wave refills every ~10
     // iterations; kept in registers it occupied scalar registers that the step's lane masks
@@ -985,8 +985,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             have = false;
         }
         if (!R.late_append) append();
-        q_event.flush_if(64, L.event, L.event_n);
-        q_emit.flush_if(64, L.emit, L.emit_n);
+        q_event.flush_if(QFLUSH, L.event, L.event_n);
+        q_emit.flush_if(QFLUSH, L.emit, L.emit_n);
 #ifdef ARTES_DEBUG_LANES
         {
             const unsigned long long bs = __ballot(dbg_s), bh = __ballot(dbg_h), bm = __ballot(dbg_m);
