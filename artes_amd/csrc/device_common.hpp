@@ -63,8 +63,8 @@ struct DevRun {
     double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
     double* __restrict__ det;       // [NCOPY][4][4][ny][nx]
     size_t det_stride;              // doubles per copy
-    double* __restrict__ tot2;      // [6] packet-level sum T^2 per Stokes, flux_emitted, flux_exit
-    unsigned long long* __restrict__ cnt;   // [ARTES_NUM_COUNTERS]
+    double* __restrict__ tot2;      // [CNT_COPIES][CNT_STRIDE] partials (tot_add) of: packet-level sum T^2 per Stokes, flux_emitted, flux_exit
+    unsigned long long* __restrict__ cnt;   // [CNT_COPIES][CNT_STRIDE] partial counters (cnt_add), summed per call
     unsigned long long* __restrict__ err;   // [ARTES_NUM_ERR]
     double* __restrict__ rec;       // [n][ARTES_TRACE_FIELDS] (TRACE builds)
     double* __restrict__ flow_g;    // [ncell][3] flow_global accumulators, or null
@@ -101,6 +101,20 @@ struct Rng {
 };
 
 __device__ __forceinline__ void log_err(const DevRun& R, int code) { atomicAdd(&R.err[code], 1ULL); }
+
+// The event counters are added once per wave at the end of every launch -- thousands of
+// same-address atomics per launch, which the memory side serialises -- so each block adds
+// into one of CNT_COPIES copies of them, 128 bytes apart (copy = block index mod 8, i.e.
+// its XCD), and the host's launch sums the copies into the caller's counters at the end
+// of the call (sum_counters, transport.hip).
+constexpr int CNT_COPIES = 8, CNT_STRIDE = 16;
+__device__ __forceinline__ void cnt_add(const DevRun& R, int k, unsigned long long v) {
+    atomicAdd(&R.cnt[(blockIdx.x % CNT_COPIES) * CNT_STRIDE + k], v);
+}
+// the same for the six per-call float totals (packet moments T^2, thermal fluxes)
+__device__ __forceinline__ void tot_add(const DevRun& R, int k, double v) {
+    unsafeAtomicAdd(&R.tot2[(blockIdx.x % CNT_COPIES) * CNT_STRIDE + k], v);
+}
 
 // sin/cos for |x| <~ 1e5 (every angle here is < 4 pi): two-constant Cody-Waite reduction
 // by pi/2 with FMA, fdlibm __kernel_sin/__kernel_cos minimax polynomials on [-pi/4, pi/4].

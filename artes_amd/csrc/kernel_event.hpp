@@ -749,8 +749,8 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
     }
     const unsigned long long ws = wave_sum_u64(c_scat), wd = wave_sum_u64(c_det);
     if ((threadIdx.x & 63) == 0) {
-        if (ws) atomicAdd(&R.cnt[ARTES_CNT_SCATTERS], ws);
-        if (wd) atomicAdd(&R.cnt[ARTES_CNT_DETECTED], wd);
+        if (ws) cnt_add(R, ARTES_CNT_SCATTERS, ws);
+        if (wd) cnt_add(R, ARTES_CNT_DETECTED, wd);
     }
 }
 
@@ -972,20 +972,20 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
                              d = wave_sum_u64(c_pkt);
     const double q0 = wave_sum_f64(t2[0]), q1 = wave_sum_f64(t2[1]), q2 = wave_sum_f64(t2[2]), q3 = wave_sum_f64(t2[3]);
     if ((threadIdx.x & 63) == 0) {
-        if (a) atomicAdd(&R.cnt[ARTES_CNT_EXITED], a);
-        if (b) atomicAdd(&R.cnt[ARTES_CNT_ABSORBED], b);
-        if (c) atomicAdd(&R.cnt[ARTES_CNT_DROPPED], c);
-        if (d) atomicAdd(&R.cnt[ARTES_CNT_PACKETS], d);
-        if (q0 != 0.0) unsafeAtomicAdd(&R.tot2[0], q0);
-        if (q1 != 0.0) unsafeAtomicAdd(&R.tot2[1], q1);
-        if (q2 != 0.0) unsafeAtomicAdd(&R.tot2[2], q2);
-        if (q3 != 0.0) unsafeAtomicAdd(&R.tot2[3], q3);
+        if (a) cnt_add(R, ARTES_CNT_EXITED, a);
+        if (b) cnt_add(R, ARTES_CNT_ABSORBED, b);
+        if (c) cnt_add(R, ARTES_CNT_DROPPED, c);
+        if (d) cnt_add(R, ARTES_CNT_PACKETS, d);
+        if (q0 != 0.0) tot_add(R, 0, q0);
+        if (q1 != 0.0) tot_add(R, 1, q1);
+        if (q2 != 0.0) tot_add(R, 2, q2);
+        if (q3 != 0.0) tot_add(R, 3, q3);
     }
     if (R.photon_source == 2) {
         const double fe = wave_sum_f64(f_emit), fx = wave_sum_f64(f_exit);
         if ((threadIdx.x & 63) == 0) {
-            if (fe != 0.0) unsafeAtomicAdd(&R.tot2[4], fe);
-            if (fx != 0.0) unsafeAtomicAdd(&R.tot2[5], fx);
+            if (fe != 0.0) tot_add(R, 4, fe);
+            if (fx != 0.0) tot_add(R, 5, fx);
         }
     }
 }

@@ -340,8 +340,8 @@ __global__ __launch_bounds__(BLOCK) void transport_kernel(DevGrid G, DevRun R) {
     const unsigned long long w_cross = wave_sum_u64(c_cross);
     if ((lane & 63) == 0) atomicAdd(&s_cnt[ARTES_CNT_CROSSINGS], w_cross);
     __syncthreads();
-    if (lane < ARTES_NUM_COUNTERS) atomicAdd(&R.cnt[lane], s_cnt[lane]);
-    if (lane < 4) unsafeAtomicAdd(&R.tot2[lane], s_tot2[lane]);
+    if (lane < ARTES_NUM_COUNTERS) cnt_add(R, lane, s_cnt[lane]);
+    if (lane < 4) tot_add(R, lane, s_tot2[lane]);
 }
 
 }  // namespace artes

@@ -1021,8 +1021,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #endif
     const unsigned long long wv = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);
     if ((threadIdx.x & 63) == 0) {
-        if (wv) atomicAdd(&R.cnt[ARTES_CNT_CROSSINGS], wv);
-        if (wp) atomicAdd(&R.cnt[ARTES_CNT_PEELS], wp);
+        if (wv) cnt_add(R, ARTES_CNT_CROSSINGS, wv);
+        if (wp) cnt_add(R, ARTES_CNT_PEELS, wp);
     }
 }
 

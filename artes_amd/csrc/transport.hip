@@ -38,6 +38,23 @@ namespace artes {
 // plane 8 counts the polarised peels, copy plane 9 the I-only ones (thermal emission,
 // surface): the reference adds the first to the counts of all four Stokes components
 // (ARTES.f90:4969-4972), the second to the count of I alone (4581, 4688)
+// add the CNT_COPIES partial event counters of a call (cnt_add) into the caller's counters
+__global__ void sum_counters(const unsigned long long* __restrict__ part, unsigned long long* __restrict__ out,
+                             const double* __restrict__ tpart, double* __restrict__ tout) {
+    const int k = threadIdx.x;
+    if (k < ARTES_NUM_COUNTERS) {
+        unsigned long long s = 0;
+#pragma unroll
+        for (int c = 0; c < CNT_COPIES; c++) s += part[c * CNT_STRIDE + k];
+        out[k] += s;
+    } else if (k >= 32 && k < 32 + 6) {   // the totals' six sums
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < CNT_COPIES; c++) s += tpart[c * CNT_STRIDE + k - 32];
+        tout[k - 32] += s;
+    }
+}
+
 __global__ void reduce_detector(const double* __restrict__ copies, size_t stride, size_t plane, double* __restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= stride) return;
@@ -83,6 +100,8 @@ struct artes_grid {
     size_t out_cap = 0;
     double* d_tot = nullptr;
     unsigned long long* d_cnt = nullptr;
+    unsigned long long* d_cnt_part = nullptr;   // [CNT_COPIES][CNT_STRIDE] per-call partial counters (cnt_add)
+    double* d_tot_part = nullptr;                // [CNT_COPIES][CNT_STRIDE] per-call partial totals (tot_add)
     unsigned long long* d_err = nullptr;
     double* d_rec = nullptr;
     size_t rec_cap = 0;
@@ -198,7 +217,7 @@ void artes_grid_destroy(artes_grid* g) {
     hipSetDevice(g->device);
     void* ptrs[] = {g->d_rf2, g->d_thetaf, g->d_tan2, g->d_phif, g->d_phis, g->d_phic, g->d_kappa, g->d_albedo, g->d_ka,
                     g->d_mats, g->d_cums, g->d_sc2, g->d_ss2, g->d_tplane, g->d_matid, g->d_copies, g->d_out,
-                    g->d_tot, g->d_cnt, g->d_err, g->d_rec, g->d_rfront, g->d_tcos, g->d_th_cdf, g->d_th_weight,
+                    g->d_tot, g->d_cnt, g->d_cnt_part, g->d_tot_part, g->d_err, g->d_rec, g->d_rfront, g->d_tcos, g->d_th_cdf, g->d_th_weight,
                     g->d_flow};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -248,6 +267,8 @@ int32_t artes_grid_create(const artes_grid_desc* desc, int32_t device, artes_gri
     HIP_TRY(upload(&g->d_tcos, T.tcos));
     HIP_TRY(hipMalloc((void**)&g->d_tot, 6 * sizeof(double)));
     HIP_TRY(hipMalloc((void**)&g->d_cnt, ARTES_NUM_COUNTERS * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc((void**)&g->d_cnt_part, CNT_COPIES * CNT_STRIDE * sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc((void**)&g->d_tot_part, CNT_COPIES * CNT_STRIDE * sizeof(double)));
     HIP_TRY(hipMalloc((void**)&g->d_err, ARTES_NUM_ERR * sizeof(unsigned long long)));
     HIP_TRY(hipEventCreate(&g->ev0));
     HIP_TRY(hipEventCreate(&g->ev1));
@@ -757,7 +778,9 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.x_max = p->x_max; R.y_max = p->y_max; R.fstop = p->fstop; R.pmin = p->photon_minimum;
     R.surface_albedo = p->surface_albedo; R.theta_star = p->theta_star; R.phi_star = p->phi_star;
     R.det = g->d_copies; R.det_stride = stride;
-    R.tot2 = tot_out; R.cnt = cnt_out; R.err = err_out; R.rec = rec;
+    R.tot2 = g->d_tot_part; R.cnt = g->d_cnt_part; R.err = err_out; R.rec = rec;
+    HIP_TRY(hipMemsetAsync(g->d_cnt_part, 0, CNT_COPIES * CNT_STRIDE * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(g->d_tot_part, 0, CNT_COPIES * CNT_STRIDE * sizeof(double), stream));
     R.flow_g = flow_g; R.flow_t = flow_t;
 
     const bool g3d = (T.ntheta > 1 || T.nphi > 1);
@@ -789,6 +812,8 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     const int rb = (int)((stride + 255) / 256);
     timed(g, ARTES_K_AUX, stream, [&] {
         hipLaunchKernelGGL(reduce_detector, dim3(rb), dim3(256), 0, stream, (const double*)g->d_copies, stride, plane, det_out);
+        hipLaunchKernelGGL(sum_counters, dim3(1), dim3(64), 0, stream, (const unsigned long long*)g->d_cnt_part, cnt_out,
+                           (const double*)g->d_tot_part, tot_out);
     });
     HIP_TRY(hipGetLastError());
     return 0;
