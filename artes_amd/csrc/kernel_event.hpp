@@ -198,8 +198,37 @@ struct TraceCursor {
     int pos, end;              // current static chunk of this wave (wave-uniform)
     int chunk, nchunk, stride; // chunk index, static chunk count, waves in the grid
     int dyn_lo, dyn_n;         // dynamic range
+    int pf;                    // list entries [.., pf) of the current chunk have their records prefetched
     bool exhausted;
 };
+
+// list index j -> list position (see Lists: j < split from the front, the rest mirrored)
+__device__ __forceinline__ int list_pos(int j, int split, int P) { return j < split ? j : P - 1 - (j - split); }
+
+// Lookahead of the static deal (k_trace).  A refill used to wait for two dependent memory
+// round trips: the list entry (the slot id), then the slot's record, a random line of the
+// pool (HBM and an address-translation miss).  Now every lane holds the slot id of one entry
+// of the wave's current static chunk (`ck_cur`, lane i: list index chunk * 64 + i) and of the
+// next one (`ck_nxt`, loaded a whole chunk ahead), so a static take reads its slot ids from
+// its own wave (ds_bpermute); and after each take the records of the chunk's next entries --
+// the next refill's -- are prefetched into L2 (`prefetch_line`), so that refill's record loads
+// hit L2 about ten iterations later.  The dynamic part still loads list entries directly.
+__device__ __forceinline__ int load_chunk(const int* list, int chunk, int nchunk, int split, int P) {
+    return chunk < nchunk ? list[list_pos(chunk * 64 + (int)(threadIdx.x & 63), split, P)] : -1;
+}
+// A load whose data nobody reads: the line (and its address translation) moves into L2.  It
+// is an LDS-DMA load (no VGPR destination, so no register can be reused under the returning
+// data) into a 256-byte LDS scratch area that nothing reads (`lds_sink`, the LDS byte address);
+// the compiler does not see it, so it places no wait for it (its own vmcnt waits only get
+// stricter: memory operations complete in issue order).  M0 is set and restored inside the
+// statement (the compiler owns it).  prefetch_drain: before the kernel ends, so no DMA write
+// lands in LDS the next block may own.
+__device__ __forceinline__ void prefetch_line(const void* p, unsigned lds_sink) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(p), "s"(lds_sink));
+}
+__device__ __forceinline__ void prefetch_drain() { asm volatile("s_waitcnt vmcnt(0)"); }
 
 __device__ __forceinline__ TraceCursor make_cursor(int n, int static_q64) {
     const int W = sub_grid() * (BLOCK / 64);            // the waves of this sub-engine
@@ -216,6 +245,7 @@ __device__ __forceinline__ TraceCursor make_cursor(int n, int static_q64) {
     c.end = (w < nchunk) ? c.pos + 64 : c.pos;
     c.dyn_lo = nchunk * 64;
     c.dyn_n = n - nchunk * 64;
+    c.pf = c.pos;
     c.exhausted = (n == 0);
     return c;
 }
@@ -231,19 +261,33 @@ __device__ __forceinline__ TraceCursor load_cursor(const TraceCursor* p) {
     c.stride = __builtin_amdgcn_readfirstlane(p->stride);
     c.dyn_lo = __builtin_amdgcn_readfirstlane(p->dyn_lo);
     c.dyn_n = __builtin_amdgcn_readfirstlane(p->dyn_n);
+    c.pf = __builtin_amdgcn_readfirstlane(p->pf);
     c.exhausted = __builtin_amdgcn_readfirstlane((int)p->exhausted) != 0;
     return c;
 }
 
-__device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, int home, bool need) {
+// Hands out up to popc(need) list indices to the lanes with `need`; returns this lane's or -1.
+// LA (k_trace's lookahead, above): a static entry's slot id comes from the chunk registers
+// (`slot`; -2: load it from the list), and the records of the chunk's next PF entries are
+// prefetched.  Call with the whole wave active.
+template <bool LA = false>
+__device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, int home, bool need, int* slot = nullptr,
+                                         int* ck_cur = nullptr, int* ck_nxt = nullptr, const Lists* L = nullptr, int split = 0,
+                                         const Slot* rec = nullptr, unsigned lds_sink = 0) {
+    constexpr int PF = 32;
     const int lane = threadIdx.x & 63;
     const unsigned long long mask = __ballot(need);
     const int k = __popcll(mask);
     const int rank = __popcll(mask & ((1ULL << lane) - 1ULL));
     int got = 0, mine = -1;
+    if constexpr (LA) *slot = -2;
     if (c.pos < c.end) {
         for (int part = 0; part < 2 && got < k && c.pos < c.end; part++) {   // current chunk, then the next
             const int take = min(k - got, c.end - c.pos);
+            if constexpr (LA) {
+                const int s = __shfl(*ck_cur, (c.pos - c.chunk * 64 + rank - got) & 63);
+                if (need && rank >= got && rank < got + take) *slot = s;
+            }
             if (need && rank >= got && rank < got + take) mine = c.pos + (rank - got);
             got += take;
             c.pos += take;
@@ -251,6 +295,20 @@ __device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, 
                 c.chunk += c.stride;
                 c.pos = c.chunk * 64;
                 c.end = (c.chunk < c.nchunk) ? c.pos + 64 : c.pos;
+                c.pf = c.pos;
+                if constexpr (LA) {
+                    *ck_cur = *ck_nxt;
+                    *ck_nxt = load_chunk(L->trace_in, c.chunk + c.stride, c.nchunk, split, L->P);
+                }
+            }
+        }
+        if constexpr (LA) {
+            // the next refill's records: entries [max(pos, pf), pos + PF) of the current chunk
+            const int lo = max(c.pos, c.pf), hi = min(c.end, c.pos + PF);
+            if (lo < hi) {
+                const int s = __shfl(*ck_cur, (lo - c.chunk * 64 + lane) & 63);
+                if (lane < hi - lo && s >= 0) prefetch_line(rec + s, lds_sink);
+                c.pf = hi;
             }
         }
         return mine;
@@ -313,7 +371,9 @@ struct WaveQueue {
         if (lane == 0) base = atomicAdd(list_n, cnt);
         base = __shfl(base, 0);
         __builtin_amdgcn_wave_barrier();
-        for (int j = lane; j < cnt; j += 64) list[base + j] = buf[j];
+#pragma unroll
+        for (int k = 0; k < QCAP / 64; k++)   // (unrolled: a counted loop here cost k_trace 18 registers and spills)
+            if (lane + 64 * k < cnt) list[base + lane + 64 * k] = buf[lane + 64 * k];
         __builtin_amdgcn_wave_barrier();
         cnt = 0;
     }

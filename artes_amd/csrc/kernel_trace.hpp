@@ -32,6 +32,11 @@ static constexpr bool TWOFACE = true;    // A/B builds: evaluate both faces of e
 #else
 static constexpr bool TWOFACE = false;
 #endif
+#ifdef ARTES_LOOKAHEAD
+static constexpr bool LOOKAHEAD = true;    // A/B builds: slot ids from the chunk registers, records prefetched (kernel_event.hpp)
+#else
+static constexpr bool LOOKAHEAD = false;   // refills load list entries and records on demand ("lookahead refills")
+#endif
 
 namespace artes {
 
@@ -438,11 +443,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     __shared__ TraceCursor s_cur[BLOCK / 64];
     TraceCursor* const my_cur = &s_cur[threadIdx.x >> 6];
     bool exhausted;
+    // the lookahead of the static deal (kernel_event.hpp, above load_chunk): the slot ids of
+    // the wave's current and next static chunk, one per lane, and the prefetches' LDS sink
+    [[maybe_unused]] int ck_cur = -1, ck_nxt = -1;
+    __shared__ int s_pf_sink[64];
+    [[maybe_unused]] const unsigned pf_sink = (unsigned)(uintptr_t)s_pf_sink;
     {
         const TraceCursor c0 = make_cursor(n, R.static_q64);
         if ((threadIdx.x & 63) == 0) *my_cur = c0;
         __builtin_amdgcn_wave_barrier();
         exhausted = c0.exhausted;
+        if constexpr (LOOKAHEAD) {
+            ck_cur = load_chunk(L.trace_in, c0.chunk, c0.nchunk, split, L.P);
+            ck_nxt = load_chunk(L.trace_in, c0.chunk + c0.stride, c0.nchunk, split, L.P);
+
+        }
     }
     const int fam_all = !G3D ? 1 : (G.nphi > 1 ? 7 : 3);
     const int nrt = G.nr * G.ntheta;        // linear-index stride of phi
@@ -719,14 +734,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             if (__popcll(idle) >= R.refill || idle == __ballot(true)) {
                 append();
                 TraceCursor cur = load_cursor(my_cur);
-                const int my = wave_take(cur, L.grab, home, !have);
+                int my;
+                if constexpr (LOOKAHEAD) {
+                    int sl;
+                    my = wave_take<true>(cur, L.grab, home, !have, &sl, &ck_cur, &ck_nxt, &L, split, S.s, pf_sink);
+                    if (!have && my >= 0) slot = sl != -2 ? sl : L.trace_in[list_pos(my, split, L.P)];
+                } else {
+                    my = wave_take(cur, L.grab, home, !have);
+                    if (!have && my >= 0) slot = L.trace_in[list_pos(my, split, L.P)];
+                }
                 if ((threadIdx.x & 63) == 0) *my_cur = cur;
                 __builtin_amdgcn_wave_barrier();
                 exhausted = cur.exhausted;
 #ifdef ARTES_DEBUG_LANES
                 dbg_refills++;
 #endif
-                if (!have && my >= 0) slot = L.trace_in[my < split ? my : L.P - 1 - (my - split)];
 #ifdef ARTES_DEBUG
                 if (!have && my >= 0) {
                     const int pos = my < split ? my : L.P - 1 - (my - split);
@@ -998,6 +1020,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     append();
     q_event.flush(L.event, L.event_n);
     q_emit.flush(L.emit, L.emit_n);
+    if constexpr (LOOKAHEAD) prefetch_drain();
 #ifdef ARTES_DEBUG_LANES
     if ((threadIdx.x & 63) == 0) {
         // (development build: error slots reused as counters, the run's error codes are void)
