@@ -34,9 +34,10 @@ def env_rank() -> Rank:
 
 
 def init(backend: str | None = None) -> Rank:
-    """Initialise torch.distributed from the torchrun environment (no-op for one process)."""
+    """Initialise torch.distributed from the torchrun environment (no-op for one process,
+    unless ARTES_DIST_FORCE=1: a one-rank group, to exercise the collective path)."""
     r = env_rank()
-    if r.world > 1:
+    if r.world > 1 or os.environ.get("ARTES_DIST_FORCE") == "1":
         import torch.distributed as dist
 
         if not dist.is_initialized():
@@ -51,8 +52,11 @@ def init(backend: str | None = None) -> Rank:
             if backend == "nccl":
                 import torch
 
-                torch.cuda.set_device(r.local_rank)
-                kw["device_id"] = torch.device("cuda", r.local_rank)
+                # (local_rank modulo the visible devices: a launcher that shows each rank only
+                # its own GPU must not make rank 3 ask for device 3)
+                d = r.local_rank % max(1, torch.cuda.device_count())
+                torch.cuda.set_device(d)
+                kw["device_id"] = torch.device("cuda", d)
             dist.init_process_group(backend=backend, rank=r.rank, world_size=r.world, **kw)
     return r
 

@@ -117,9 +117,12 @@ def main() -> int:
     err = torch.zeros(64, dtype=torch.int64, device=f"cuda:{dev}")
     stream = torch.cuda.current_stream()
     backend = None
-    if world > 1:
-        import torch.distributed as tdist
-
+    # the collective path (the step's all_reduce, the max-over-ranks timing, the barriers) runs
+    # with more than one rank, or at one rank when ARTES_DIST_FORCE=1 initialised a process
+    # group anyway (dist.init): RCCL's one-rank rehearsal of that path on a one-GPU box
+    import torch.distributed as tdist
+    coll = world > 1 or (tdist.is_available() and tdist.is_initialized())
+    if coll:
         backend = tdist.get_backend()
 
     def step(k: int):
@@ -127,21 +130,21 @@ def main() -> int:
         first = (k * world + r.rank) * per_gpu
         grid.run_device(params, first, per_gpu, args.seed, det.data_ptr(), tot2.data_ptr(), cnt.data_ptr(),
                         err.data_ptr(), stream.cuda_stream)
-        if world > 1:
+        if coll:
             flat[n_det + 6:n_det + 14].copy_(cnt)
             flat[n_det + 14:].copy_(err)
             tdist.all_reduce(flat)
 
     def counts():
         """(counters, error codes) of the last step, summed over ranks."""
-        if world > 1:
+        if coll:
             return (flat[n_det + 6:n_det + 14].cpu().numpy().astype(np.float64),
                     np.rint(flat[n_det + 14:].cpu().numpy()).astype(np.int64))
         return cnt.cpu().numpy().astype(np.float64), err.cpu().numpy()
 
     def barrier():
         torch.cuda.synchronize()
-        if world > 1:
+        if coll:
             tdist.barrier()
         torch.cuda.synchronize()
 
@@ -169,13 +172,13 @@ def main() -> int:
     step_ms = [a.elapsed_time(b) for a, b in ev]
     ktimes = grid.kernel_times()   # {class: (summed ms over the timed steps, launches)}
     grid.set_profiling(False)
-    if world > 1:
+    if coll:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     cnt_h, err_h = counts()
     if r.rank != 0:
-        if world > 1:
+        if coll:
             tdist.barrier()
         return 0
 
@@ -312,7 +315,7 @@ def main() -> int:
         "errors": err_rate,
     }
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if coll:
         tdist.barrier()
     return 0
 
