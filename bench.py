@@ -64,6 +64,12 @@ def _md5(path: str) -> str | None:
 
 
 def main() -> int:
+    # stdout carries exactly one JSON line (rank 0): libraries that print to the process's
+    # descriptor 1 -- RCCL writes its version banner there when a communicator starts -- are
+    # pointed at stderr, and the line is written to the saved descriptor
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -314,7 +320,7 @@ def main() -> int:
         # reference error codes (error.log numbers) logged in the timed steps, with their rate
         "errors": err_rate,
     }
-    print(json.dumps(out), flush=True)
+    os.write(json_fd, (json.dumps(out) + "\n").encode())
     if coll:
         tdist.barrier()
     return 0
