@@ -368,13 +368,19 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     // moving towards it (3066-3070, 3116-3118)
     // (the chosen face's rules as outer (ch) or inner face: flag bits 1 / 2 and 4 / 5; a
     // quadratic's two roots are on one face, so they share them)
-    const int fsh = ch ? 0 : 1;
+    // (one AND of the flags with the bits that apply -- the role's two when the packet sits
+    // on the face, the edge bit always -- then a test per rule: integer selects of constants,
+    // where per-rule bit extractions cost lane-mask/VGPR conversions)
+    // (radial-only grids: the sphere's rules, 1e-3 m as outer face, the veto as inner face)
+    const int fsel = (sameA & !isP) ? (ch ? (FR_KS_OUT | FR_BIG_OUT) : (FR_KS_IN | FR_BIG_IN)) : 0;
+    const int fhit = fl & (fsel | FR_EDGE);
     const double A = pl ? zp : rA;
-    const bool big = !isP & sameA & ((fl >> (4 + fsh)) & 1);
-    vA = (vA & !pl & (A > K.tol) & (!big | (A > K.tol_same))) | (pl & (ch ? (n2 < -K.tol) : (n2 > K.tol)) & (A > 0.0));
+    const bool big = G3D ? (fhit & (FR_BIG_OUT | FR_BIG_IN)) != 0 : sameA & ch;
+    const double n2s = ch ? -n2 : n2;   // (moving towards the plane: n2 < 0 as outer face, > 0 as inner)
+    vA = (vA & !pl & (A > K.tol) & (!big | (A > K.tol_same))) | (pl & (n2s > K.tol) & (A > 0.0));
     vB = vB & !pl & (rB > K.tol) & (!big | (rB > K.tol_same));
     // vetoes (ARTES.f90:2899-2960, 3014-3290, 3318, 3346)
-    const bool qkill = (fl & FR_EDGE) | (sameA & ((fl >> (1 + fsh)) & 1));
+    const bool qkill = G3D ? (fhit & (FR_EDGE | FR_KS_OUT | FR_KS_IN)) != 0 : sameA & !ch;
     const bool sp0_big = !sameA & (fabs(den0) > 0.0) & !(rA < K.huge);
     const bool killA = isP ? sameA : qkill;
     const bool killB = isP ? (sameB | sp0_big) : qkill;
@@ -822,7 +828,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 e0 = fam == 0 ? dm : e0;
                 e1 = fam == 1 ? dm : e1;
                 e2 = fam == 2 ? dm : e2;
-                sides = (sides & ~(0x11 << fam)) | ((outer ? 1 : 0) << fam) | ((retry ? 1 : 0) << (4 + fam));
+                sides = (sides & ~(0x11 << fam)) | (((outer ? 1 : 0) | (retry ? 16 : 0)) << fam);
             } else {
                 e0 = dm;
                 sides = (outer ? 1 : 0) | ((retry ? 1 : 0) << 4);
