@@ -328,7 +328,8 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
         // as a plain hb*hb - qa*qc the compiler contracts it into an FMA of its own choosing,
         // and a grazing ray could then see the inner sphere here but not there, or back)
         const bool in_ok = (hb < 0.0) & (fma(hb, hb, -(qa_in * qc_in)) >= 0.0) & !same_in;
-        ch = isT ? (fma(n2, Cxy + Cz, -z * hb) < 0.0) : !in_ok;
+        const bool t_out = fma(n2, Cxy + Cz, -z * hb) < 0.0;
+        ch = (isT & t_out) | (!isT & !in_ok);   // (as masks: no branch around the radial record's read)
         ch = ch != alt;
     }
     const FaceRec fc = T.fr[e + (ch ? 1 : 0)];
@@ -377,8 +378,9 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     const double A = pl ? zp : rA;
     const bool big = G3D ? (fhit & (FR_BIG_OUT | FR_BIG_IN)) != 0 : sameA & ch;
     const double n2s = ch ? -n2 : n2;   // (moving towards the plane: n2 < 0 as outer face, > 0 as inner)
-    vA = (vA & !pl & (A > K.tol) & (!big | (A > K.tol_same))) | (pl & (n2s > K.tol) & (A > 0.0));
-    vB = vB & !pl & (rB > K.tol) & (!big | (rB > K.tol_same));
+    const double tmin = big ? K.tol_same : K.tol;   // (one threshold per lane: two compares fewer in the mask logic)
+    vA = (vA & !pl & (A > tmin)) | (pl & (n2s > K.tol) & (A > 0.0));
+    vB = vB & !pl & (rB > tmin);
     // vetoes (ARTES.f90:2899-2960, 3014-3290, 3318, 3346)
     const bool qkill = G3D ? (fhit & (FR_EDGE | FR_KS_OUT | FR_KS_IN)) != 0 : sameA & !ch;
     const bool sp0_big = !sameA & (fabs(den0) > 0.0) & !(rA < K.huge);
@@ -918,10 +920,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     }
                 }
 #endif
-                if (err) {   // (one rarely taken branch for the three error codes)
+                // (the error codes are logged on the chain-end paths below: every error stops)
+                auto log_step_err = [&]() {
                     if (runaway) log_err(R, ARTES_ERR_RUNAWAY);
                     log_err(R, err31 ? 31 : 34);
-                }
+                };
                 ncross++;
                 const double tau_cell = best * k;
                 const bool prop = (mode == S_PROP);
@@ -958,6 +961,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     parked = 4;
                 } else if (prop) {
                     if (err) {
+                        log_step_err();
                         log_err(R, 3);
                         end = S_END_DROP;
                     } else if (exit) {                             // left the atmosphere
@@ -982,7 +986,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 } else {   // a first-optical-depth or peel-off trace reached the boundary
                     tacc += tau_cell;
                     // error codes of the four traces (ARTES.f90:640, 4743, 4549, 4653)
-                    if (err) log_err(R, mode == S_FIRST ? 2 : mode == S_PEEL ? 43 : mode == S_PEEL_T ? 46 : 42);
+                    if (err) {
+                        log_step_err();
+                        log_err(R, mode == S_FIRST ? 2 : mode == S_PEEL ? 43 : mode == S_PEEL_T ? 46 : 42);
+                    }
                     if (is_peel_trace(mode)) {
                         const int kind = mode == S_PEEL_T ? 1 : mode == S_PEEL_S ? 2 : 0;
                         end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0) | (kind << PEEL_KIND_SHIFT);
