@@ -825,7 +825,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
                 retry = (fam != 2) & !alt & !(dm < K.inf);
             }
-            if constexpr (LAZY) dm = retry ? 0.0 : dm;   // (the other face is still to come: no bound)
+            // (the other face is still to come: no bound.  Only the high word is cleared: the
+            // entry is then 0 or a positive denormal, below any step, so the family stays the
+            // nearest pending one exactly as with 0)
+            if constexpr (LAZY) dm = __hiloint2double(retry ? 0 : __double2hiint(dm), __double2loint(dm));
             if constexpr (G3D) {
                 e0 = fam == 0 ? dm : e0;
                 e1 = fam == 1 ? dm : e1;
