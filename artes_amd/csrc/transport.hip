@@ -331,15 +331,15 @@ static int32_t wl_set(artes_grid* g, int wl, artes_grid::WlSet** out) {
         HIP_TRY(upload(&W.d_mats, mats));
         HIP_TRY(upload(&W.d_cums, cums));
         // the block-diagonal form of spheres and Rayleigh scattering, value by value (interp_matrix):
-        // k_event then reads 4 of the 16 elements per row (ARTES_MSYM=0 turns it off)
+        // k_event then reads 4 of the 16 elements per row (built whenever the matrices qualify;
+        // launch() reads ARTES_MSYM=0 per call to use the 16-element form instead)
         bool sym = true;
         for (size_t k = 0; k < mats.size() && sym; k += NELEM) {
             const double* m = &mats[k];
             sym = m[2] == 0.0 && m[3] == 0.0 && m[6] == 0.0 && m[7] == 0.0 && m[8] == 0.0 && m[9] == 0.0 && m[12] == 0.0 &&
                   m[13] == 0.0 && m[4] == m[1] && m[5] == m[0] && m[15] == m[10] && m[14] == -m[11];
         }
-        const char* ms = getenv("ARTES_MSYM");
-        if (sym && !(ms && atoi(ms) == 0)) {
+        if (sym) {
             std::vector<double> m4(ids.size() * NANG * 4);
             for (size_t r = 0; r < ids.size() * NANG; r++) {
                 const double* m = &mats[r * NELEM];
@@ -721,8 +721,9 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
         const int32_t rc = wl_set(g, p->wl_index, &W);
         if (rc) return rc;
         G.nmat = W->nmat; G.matid = W->d_matid; G.cums = W->d_cums;
-        // (the persistent engine reads the 16-element form)
-        G.msym = (W->d_mats4 && use_event_engine()) ? 1 : 0;
+        // (the persistent engine reads the 16-element form; ARTES_MSYM=0, read per call, too)
+        const char* ms = getenv("ARTES_MSYM");
+        G.msym = (W->d_mats4 && use_event_engine() && !(ms && atoi(ms) == 0)) ? 1 : 0;
         G.mats = G.msym ? W->d_mats4 : W->d_mats;
     }
     G.sc2 = g->d_sc2; G.ss2 = g->d_ss2;
@@ -792,7 +793,13 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
             return fail(-22, "event engine addresses the per-cell table with 32-bit byte offsets: ncell < 2^28");
         int32_t rc = g3d ? run_event_engine<true>(g, G, R, rec != nullptr, stream)
                          : run_event_engine<false>(g, G, R, rec != nullptr, stream);
-        if (rc) return rc;
+        if (rc) {
+            // the counters and totals of what did run still reach the caller (a failed run's
+            // error codes are already in err_out): fold the partials before reporting the failure
+            hipLaunchKernelGGL(sum_counters, dim3(1), dim3(64), 0, stream, (const unsigned long long*)g->d_cnt_part,
+                               cnt_out, (const double*)g->d_tot_part, tot_out);
+            return rc;
+        }
     } else if (n > 0) {
         uint64_t want = (n + BLOCK - 1) / BLOCK;
         int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)g->max_blocks));

@@ -33,6 +33,17 @@ def env_rank() -> Rank:
                 int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def device_of(r: Rank) -> int:
+    """The HIP device of rank ``r``: ``local_rank`` modulo the visible devices.  One rule for
+    every entry point (``init``'s RCCL device, ``bench.py``, the drop-in CLI): a launcher that
+    shows each rank only its own GPU must not make rank 3 ask for device 3, and ranks sharing
+    one card (the gloo rehearsal on a one-GPU box) all use device 0.  Counting devices does
+    not initialise the GPU on this image."""
+    import torch
+
+    return r.local_rank % max(1, torch.cuda.device_count())
+
+
 def init(backend: str | None = None) -> Rank:
     """Initialise torch.distributed from the torchrun environment (no-op for one process,
     unless ARTES_DIST_FORCE=1: a one-rank group, to exercise the collective path)."""
@@ -52,9 +63,7 @@ def init(backend: str | None = None) -> Rank:
             if backend == "nccl":
                 import torch
 
-                # (local_rank modulo the visible devices: a launcher that shows each rank only
-                # its own GPU must not make rank 3 ask for device 3)
-                d = r.local_rank % max(1, torch.cuda.device_count())
+                d = device_of(r)
                 torch.cuda.set_device(d)
                 kw["device_id"] = torch.device("cuda", d)
             dist.init_process_group(backend=backend, rank=r.rank, world_size=r.world, **kw)

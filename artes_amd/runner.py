@@ -134,10 +134,11 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
     det = driver.detector_geometry(cfg, r_top)
     if seed is None:   # the reference's clock seed (ARTES.f90:4187), drawn once on rank 0
         seed = dist.broadcast_int(int(time.time() * 1e6) & 0x7FFFFFFFFFFFFFFF, r)
+    device = dist.device_of(r)
     if transport_factory is None:
-        transport = Transport(atm, device=r.local_rank, oblateness=cfg.oblateness)
+        transport = Transport(atm, device=device, oblateness=cfg.oblateness)
     else:
-        transport = transport_factory(atm, r.local_rank, cfg.oblateness)
+        transport = transport_factory(atm, device, cfg.oblateness)
     if r.rank == 0:
         driver.write_plot_dat(run_dir, cfg, float(atm["radial"][0]), ntheta, det.x_fov)
     wavelengths = np.asarray(atm["wavelength"], dtype=np.float64) * 1.0e-6

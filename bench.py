@@ -36,22 +36,56 @@ B_PER_CROSSING, B_PER_SCATTER, B_PER_PEEL = 8.0, 304.0, 352.0
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 
 
-def cpu_baseline(atm, params, budget_s: float = 15.0) -> dict:
-    """The CPU oracle (C restatement of the reference packet loop, OpenMP) on host cores."""
+def host_cores() -> dict:
+    """The host cores this process may use: the affinity mask, capped by the cgroup's CPU
+    quota when one is set (a container's share of a larger machine), and the machine's count."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:                                       # cgroup v2
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        try:                                   # cgroup v1
+            q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            if q > 0:
+                quota = q / float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        except (OSError, ValueError):
+            pass
+    usable = affinity if quota is None else max(1, min(affinity, int(math.ceil(quota))))
+    return {"visible": os.cpu_count() or 1, "affinity": affinity,
+            "cgroup_quota": None if quota is None else round(quota, 2), "usable": usable}
+
+
+def cpu_baseline(atm, params, budget_s: float = 15.0, single_s: float = 4.0) -> dict:
+    """The CPU oracle (C restatement of the reference packet loop, OpenMP) on every host core
+    this process may use (``ARTES_CPU_THREADS`` overrides), plus a one-thread rate: DESIGN.md
+    §6 calibrates the port against the reference per core (1.2-1.5x)."""
     from oracle import oracle
 
-    threads = int(os.environ.get("ARTES_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    cores = host_cores()
+    threads = int(os.environ.get("ARTES_CPU_THREADS", cores["usable"]))
     g = oracle.OracleGrid(atm)
-    probe = 20000
-    t0 = time.perf_counter()
-    g.run(params, 0, probe, 99, threads=threads)
-    rate = probe / max(time.perf_counter() - t0, 1e-6)
-    n = int(min(max(rate * budget_s, 1e5), 5e7))
-    t0 = time.perf_counter()
-    g.run(params, 10**12, n, 99, threads=threads)
-    dt = time.perf_counter() - t0
+
+    def rate(first, threads, budget):
+        probe = 2000 * threads
+        t0 = time.perf_counter()
+        g.run(params, first, probe, 99, threads=threads)
+        r = probe / max(time.perf_counter() - t0, 1e-6)
+        n = int(min(max(r * budget, 2e4), 5e7))
+        t0 = time.perf_counter()
+        g.run(params, first + probe, n, 99, threads=threads)
+        dt = time.perf_counter() - t0
+        return n, dt
+
+    n, dt = rate(10**12, threads, budget_s)
+    n1, dt1 = rate(2 * 10**12, 1, single_s)
     return {"value": round(n / dt / 1e6, 4), "unit": "Mphotons/s", "cores": threads, "kind": "port",
-            "sample": f"{n} packets of the same ray3d workload (oracle/artes_oracle.c, {threads} OpenMP threads, {dt:.1f} s)"}
+            "cores_visible": cores["visible"], "cores_affinity": cores["affinity"],
+            "cgroup_cpu_quota": cores["cgroup_quota"],
+            "one_thread": {"value": round(n1 / dt1 / 1e6, 5), "unit": "Mphotons/s", "packets": n1, "seconds": round(dt1, 2)},
+            "sample": f"{n} packets of the same ray3d workload (oracle/artes_oracle.c, {threads} OpenMP threads, {dt:.1f} s; "
+                      f"threads = the affinity mask's cores capped by the cgroup CPU quota)"}
 
 
 def _md5(path: str) -> str | None:
@@ -93,7 +127,7 @@ def main() -> int:
     world = r.world
     # one GPU per rank; more ranks than devices only in a gloo rehearsal (ARTES_DIST_BACKEND=gloo),
     # since RCCL refuses two ranks on one device
-    dev = r.local_rank % max(1, torch.cuda.device_count())
+    dev = dist.device_of(r)
     torch.cuda.set_device(dev)
     per_gpu = int(args.packets)
 

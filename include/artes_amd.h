@@ -31,7 +31,13 @@
  *     Lambertian surface, 4600-4708) add their count to the Stokes-I count alone,
  *     as the reference does.
  *   - Functions return 0 on success or a negative errno-style code; they never
- *     exit the process (the reference calls exit(0) on fatal errors).
+ *     exit the process (the reference calls exit(0) on fatal errors).  A failed
+ *     run still reports the counters and totals of the packets it did transport.
+ *   - One call at a time per grid handle: the packet pool, the work lists and the
+ *     per-call partial counters belong to the handle, so two artes_run_device calls
+ *     on one grid from different streams must be ordered by the caller (one stream,
+ *     or an event between them).  Separate handles are independent (several engines
+ *     can share a device, each on its own stream).
  *   - Error-code counters: uint64_t err[ARTES_NUM_ERR], index = the reference's
  *     "error NNN" number written to error.log (e.g. ARTES.f90:640, 3401).  Two
  *     indices the reference does not use report engine faults, after which the run's

@@ -92,7 +92,7 @@ def test_crossing_counter_is_sum_of_packet_crossings(require_gpu, name, spec):
     atm, grid, p = _setup(name, **spec)
     rec = grid.trace(p, 0, 50000, 12)
     c = grid.run(p, 0, 50000, 12).counter("crossings")
-    assert c == pytest.approx(rec[:, 2].sum(), rel=1e-4)
+    assert c == int(rec[:, 2].sum())
 
 
 def test_packet_moments_are_pure_diagnostics(require_gpu):
