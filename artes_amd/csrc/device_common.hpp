@@ -60,6 +60,7 @@ struct DevRun {
     double photon_bias;
     double det0, det1, det2, sdt, cdt, sdp, cdp;
     double det_phi;                 // atan2(det1, det0) in [0, 2 pi] (peel_photon, ARTES.f90:4868-4870)
+    double cdphi, sdphi;            // its cosine and sine
     double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
     double* __restrict__ det;       // [NCOPY][4][4][ny][nx]
     size_t det_stride;              // doubles per copy
@@ -305,22 +306,26 @@ __device__ __forceinline__ void mueller(double psi, double& c2p, double& s2p) {
         s2p = -s2p;
 }
 
-// polarization_rotation (ARTES.f90:1663-1932); sc is scatter(4,4) row-major.  c2b / s2b:
-// mueller(beta), when the caller has it already (the scattering path: sample_angles computed
-// it for the same beta), else computed here (HAVE_CS = false)
-template <bool HAVE_CS = false>
-__device__ void polarization_rotation(const DevRun& R, double alpha, double beta, const double si[4],
-                                      const double sc[16], double d2, double dn2, double so[4], bool peeling,
-                                      double c2b = 0.0, double s2b = 0.0) {
+// polarization_rotation (ARTES.f90:1663-1932); sc is scatter(4,4) row-major.  The first
+// rotation is mueller(beta) = (c2b, s2b) (ARTES.f90:1934-1960), and beta's half-turn decides
+// the rotation back: rot_lo = beta in [0, pi), rot_hi = beta in [pi, 2 pi) (neither: none).
+// The angle back, beta2 = acos(num) (1730-1751), is used only through mueller(+-beta2), i.e.
+// cos(2 beta2) = 2 num^2 - 1 and the sine's sign by beta2's quadrant, which is num's sign
+// (beta2 in (pi/2, pi) <=> num in (-1, 0)): no acos and no cosine of the angle.  (The
+// reference rounds through the angle; the two agree to ~1e-16 absolute, except that the
+// quadrant test sees num's sign where the rounded acos(num) may land on pi/2 for
+// |num| < 1e-16.)
+__device__ void polarization_rotation_cs(const DevRun& R, double alpha, double c2b, double s2b, bool rot_lo, bool rot_hi,
+                                         const double si[4], const double sc[16], double d2, double dn2, double so[4],
+                                         bool peeling) {
     if (fabs(alpha) < 1.0 && fabs(dn2) < 1.0) {
-        double beta2 = 0.0;
+        double x2 = 1.0;   // cos(beta2); beta2 = 0 unless set (ARTES.f90:1730-1751)
         const double num = (d2 - dn2 * alpha) / (dsqrt(1.0 - alpha * alpha) * dsqrt(1.0 - dn2 * dn2));
-        if (fabs(num) <= 1.0) beta2 = acos(num);
-        else if (num > 1.0 && num < 1.00001) beta2 = 0.0;
-        else if (num < -1.0 && num > -1.00001) beta2 = PI;
+        if (fabs(num) <= 1.0) x2 = num;
+        else if (num > 1.0 && num < 1.00001) x2 = 1.0;
+        else if (num < -1.0 && num > -1.00001) x2 = -1.0;   // beta2 = pi
         else log_err(R, 11);
         double c = c2b, s = s2b;
-        if constexpr (!HAVE_CS) mueller(beta, c, s);
         double r0 = si[0], r1 = c * si[1] + s * si[2], r2 = -s * si[1] + c * si[2], r3 = si[3];
         const double pr = dsqrt(r1 * r1 + r2 * r2 + r3 * r3);
         double norm = (pr > 0.0) ? dsqrt(si[1] * si[1] + si[2] * si[2] + si[3] * si[3]) / pr : 1.0;
@@ -337,15 +342,13 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
                 log_err(R, 12);
             }
         }
-        // mueller(beta2) or mueller(-beta2) (ARTES.f90:1905-1910): the same cosine bit for bit
-        // (sincos_bounded is odd/even exactly), so one evaluation, no divergent pair; the sign
-        // of the sine by mueller_matrix_filler's quadrant rule for +beta2 or -beta2 (beta2 in
-        // [0, pi]: negative on (pi/2, pi) for +beta2, on (0, pi/2) for -beta2)
-        const bool rot_lo = beta >= 0.0 && beta < PI, rot_hi = beta >= PI && beta < TWO_PI;
+        // mueller(beta2) or mueller(-beta2) (ARTES.f90:1905-1910): cos(2 beta2) either way; the
+        // sine negative on beta2 in (pi/2, pi) for +beta2 (num in (-1, 0)), on (0, pi/2) for
+        // -beta2 (num in (0, 1))
         if (rot_lo || rot_hi) {
-            const double c2 = cos_b(2.0 * beta2);
+            const double c2 = fma(2.0 * x2, x2, -1.0);
             const double s2 = dsqrt(1.0 - c2 * c2);
-            const bool neg = rot_lo ? (beta2 > HALF_PI && beta2 < PI) : (beta2 > 0.0 && beta2 < HALF_PI);
+            const bool neg = rot_lo ? (x2 < 0.0 && x2 > -1.0) : (x2 > 0.0 && x2 < 1.0);
             c = c2;
             s = neg ? -s2 : s2;
         }
@@ -380,22 +383,44 @@ __device__ void polarization_rotation(const DevRun& R, double alpha, double beta
     }
 }
 
+// the same with the first rotation given by its angle beta (mueller(beta) computed here unless
+// HAVE_CS: the scattering path's sample_angles computed it for the same beta)
+template <bool HAVE_CS = false>
+__device__ __forceinline__ void polarization_rotation(const DevRun& R, double alpha, double beta, const double si[4],
+                                                      const double sc[16], double d2, double dn2, double so[4], bool peeling,
+                                                      double c2b = 0.0, double s2b = 0.0) {
+    if constexpr (!HAVE_CS) mueller(beta, c2b, s2b);
+    polarization_rotation_cs(R, alpha, c2b, s2b, beta >= 0.0 && beta < PI, beta >= PI && beta < TWO_PI, si, sc, d2, dn2, so,
+                             peeling);
+}
+
 // the azimuth of direction (d0, d1) in [0, 2 pi) as direction_cosine takes it (ARTES.f90:1975-1977)
 __device__ __forceinline__ double azimuth(double d0, double d1) {
     double phi = atan2(d1, d0);
     if (phi < 0.0) phi += TWO_PI;
     return phi;
 }
+// its cosine and sine without the angle: (d0, d1) / |(d0, d1)|, and (1, 0) for d0 = d1 = 0
+// (atan2(0, 0) = 0)
+__device__ __forceinline__ void azimuth_cs(double d0, double d1, double& c, double& s) {
+    const double rho = dsqrt(d0 * d0 + d1 * d1);
+    const double inv = rho > 0.0 ? 1.0 / rho : 0.0;
+    c = rho > 0.0 ? d0 * inv : 1.0;
+    s = d1 * inv;
+}
 
-// direction_cosine (ARTES.f90:1962-2052); phi_old = azimuth(d0, d1), when the caller has it
-// already (k_event: the peel-off needed the same azimuth), else computed here
-template <bool HAVE_PHI = false>
-__device__ void direction_cosine(const DevRun& R, double alpha, double beta, double d0, double d1, double d2,
-                                 double& e0, double& e1, double& e2, double phi_in = 0.0) {
+// direction_cosine (ARTES.f90:1962-2052) with the old direction's azimuth given as its
+// cosine and sine (cpo, spo).  The new azimuth phi_old -+ acos(num) is used only through
+// its cosine and sine (2030-2050), so they follow from the angle-sum rule with
+// cos(acos(num)) = num and sin(acos(num)) = sqrt(1 - num^2) >= 0: no atan2, acos or cosine
+// of the angle.  The reference takes the sine as +-sqrt(1 - cos^2) by phi_new's half-turn,
+// the same value up to rounding (its sign is sin(phi_new)'s); the error paths keep their
+// phi_new = 0, i.e. (cos, sin) = (1, 0).
+__device__ void direction_cosine_cs(const DevRun& R, double alpha, double beta, double d0, double d1, double d2,
+                                    double cpo, double spo, double& e0, double& e1, double& e2) {
     const double cto = d2 / dsqrt(d0 * d0 + d1 * d1 + d2 * d2);
     const double sto = dsqrt(1.0 - cto * cto);
-    const double phi_old = HAVE_PHI ? phi_in : azimuth(d0, d1);
-    double ctn = 0.0, phi_new = 0.0, spn = 0.0;
+    double ctn = 0.0;
     const bool upper = (beta >= PI && beta < TWO_PI);
     const bool lower = (beta >= 0.0 && beta < PI);
     // (one cosine of the branch's argument: the same value, no divergent pair)
@@ -406,23 +431,36 @@ __device__ void direction_cosine(const DevRun& R, double alpha, double beta, dou
     double num = (alpha - ctn * cto) / (stn * sto);
     if (num >= 1.0) num = 1.0 - 1.e-10;
     else if (num <= -1.0) num = -1.0 + 1.e-10;
+    double cpn = 1.0, spn = 0.0;
     if (fabs(num) <= 1.0) {
-        const double an = acos(num);
-        if (upper) phi_new = phi_old - an;
-        else if (lower) phi_new = phi_old + an;
-        else log_err(R, 19);
+        if (upper || lower) {
+            const double san = dsqrt(1.0 - num * num);
+            const double sg = upper ? -san : san;   // phi_new = phi_old - acos(num) (upper), + (lower)
+            cpn = cpo * num - spo * sg;
+            spn = spo * num + cpo * sg;
+        } else {
+            log_err(R, 19);
+        }
     } else {
         log_err(R, 20);
     }
-    if (phi_new < 0.0) phi_new += TWO_PI;
-    if (phi_new > TWO_PI) phi_new -= TWO_PI;
-    const double cpn = cos_b(phi_new);
-    if (phi_new >= 0.0 && phi_new < PI) spn = dsqrt(1.0 - cpn * cpn);
-    else if (phi_new >= PI && phi_new <= TWO_PI) spn = -dsqrt(1.0 - cpn * cpn);
-    else log_err(R, 21);
     e0 = stn * cpn;
     e1 = stn * spn;
     e2 = ctn;
+}
+
+// the same with the azimuth computed here (or given as the angle phi_in, HAVE_PHI)
+template <bool HAVE_PHI = false>
+__device__ __forceinline__ void direction_cosine(const DevRun& R, double alpha, double beta, double d0, double d1, double d2,
+                                                 double& e0, double& e1, double& e2, double phi_in = 0.0) {
+    double cpo, spo;
+    if constexpr (HAVE_PHI) {
+        cpo = cos_b(phi_in);
+        spo = sin_b(phi_in);
+    } else {
+        azimuth_cs(d0, d1, cpo, spo);
+    }
+    direction_cosine_cs(R, alpha, beta, d0, d1, d2, cpo, spo, e0, e1, e2);
 }
 
 // linear interpolation of the 16 elements at angle acos(mu) between bin centres
@@ -434,8 +472,7 @@ __device__ void direction_cosine(const DevRun& R, double alpha, double beta, dou
 // (the duplicated elements interpolate identically, the zeros to +0, and -P34's
 // interpolation is the exact negative of P34's).
 template <int RS = 16, int RS4 = 4>
-__device__ __forceinline__ void interp_matrix(const double* __restrict__ P, bool sym, double acos_mu, double sc[16]) {
-    const double deg = acos_mu * 180.0 / PI;
+__device__ __forceinline__ void interp_matrix_deg(const double* __restrict__ P, bool sym, double deg, double sc[16]) {
     const int ideg = (int)deg;
     int up, lo;
     if (deg - (double)ideg > 0.5) { up = ideg + 2; lo = ideg + 1; }
@@ -474,6 +511,12 @@ __device__ __forceinline__ void interp_matrix(const double* __restrict__ P, bool
 #pragma unroll
         for (int i = 0; i < 16; i++) sc[i] = (x1[i] - x0[i]) * f + x0[i];
     }
+}
+
+// the same at angle acos(mu) (ARTES.f90:1448-1450: the angle in degrees)
+template <int RS = 16, int RS4 = 4>
+__device__ __forceinline__ void interp_matrix(const double* __restrict__ P, bool sym, double acos_mu, double sc[16]) {
+    interp_matrix_deg<RS, RS4>(P, sym, acos_mu * 180.0 / PI, sc);
 }
 
 // smallest i in [1,180] with C(i) >= s for a non-decreasing C given by `cdf(i)`
@@ -515,7 +558,8 @@ __device__ __forceinline__ int cdf_search4(double s, F cdf) {
 // C = [181][CS] (CS = 4, or 5 in LDS: see k_event)
 template <int CS = 4>
 __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* __restrict__ C, Rng& rng,
-                              const double st[4], double& alpha, double& beta, double& c2b, double& s2b) {
+                              const double st[4], double& alpha, double& beta, double& c2b, double& s2b,
+                              double* adeg_out = nullptr) {
     // azimuth: C_b(i) = i (p11 I + p14 V) + (p12 Q + p13 U) SC2(i) + (p12 U - p13 Q) SS2(i)
     const double p11 = C[180 * CS + 0], p12 = C[180 * CS + 1], p13 = C[180 * CS + 2], p14 = C[180 * CS + 3];
     const double u = p11 * st[0] + p14 * st[3];
@@ -542,6 +586,7 @@ __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* _
     y0 = ct(i - 1);
     y1 = ct(i);
     const double adeg = (s - y0) / (y1 - y0) + (double)(i - 1);
+    if (adeg_out) *adeg_out = adeg;
     alpha = cos_b(adeg * PI / 180.0);
     if (fabs(alpha) >= 1.0) log_err(R, 56);
     if (alpha >= 1.0) alpha = 1.0 - 1.e-10;

@@ -582,9 +582,10 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         const bool sym = G.msym != 0;
         const double* __restrict__ P = G.mats + (size_t)mid * (sym ? TL::MAT4 : TL::MAT);
         const double tau_peel = L0.tpeel;
-        // the incoming direction's azimuth: the peel-off's phi_old (ARTES.f90:4868-4870) and the
-        // scattering's (direction_cosine, 1975-1977) -- one atan2 for both
-        const double phi_old = azimuth(dx, dy);
+        // the incoming direction's azimuth, as its cosine and sine (azimuth_cs): the peel-off's
+        // phi_old (ARTES.f90:4868-4870) and the scattering's (direction_cosine, 1975-1977)
+        double cpo, spo;
+        azimuth_cs(dx, dy, cpo, spo);
         bool drop = false;
         if ((m & FLAG_EXIT) && tau_peel < 50.0) {
             const double w = exp(-tau_peel);
@@ -593,21 +594,30 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             else if (mu <= -1.0) mu = -1.0 + 1.e-10;
             double sc[16];
             interp_matrix<TL::RS, TL::RS4>(P, sym, acos(mu), sc);
-            const double phi_new = R.det_phi;   // the detector's azimuth, once per run
             bool have_out = false;
             double so[4] = {0, 0, 0, 0};
             if (fabs(dz) < 1.0) {
+                // the rotation angle phs (4872-4916) = acos(num), or its clamps 1e-10 / pi - 1e-10
+                // (0 for a NaN), turned to 2 pi - phs when (phi_old - phi_det) mod 2 pi lies in
+                // [0, pi).  It enters polarization_rotation only through mueller(phs) and its
+                // half-turn: cos(2 phs) = 2 x^2 - 1 (x = num, or +-1 at the clamps, where the
+                // reference's cos(2 phs) rounds to 1), the sine negative on phs in (pi/2, pi)
+                // (x < 0) and on (3 pi/2, 2 pi) (turned, x > 0); no acos and no cosine
                 const double num = (R.det2 - dz * mu) / (dsqrt(1.0 - mu * mu) * dsqrt(1.0 - dz * dz));
-                double phs = 0.0;
-                if (fabs(num) < 1.0) phs = acos(num);
-                else if (num >= 1.0) phs = 1.e-10;
-                else if (num <= -1.0) phs = PI - 1.e-10;
-                else log_err(R, 44);
-                if (phi_old - phi_new >= 0.0 && phi_old - phi_new < PI) phs = TWO_PI - phs;
-                if (TWO_PI + phi_old - phi_new >= 0.0 && TWO_PI + phi_old - phi_new < PI) phs = TWO_PI - phs;
-                if (phs < 0.0) phs += TWO_PI;
+                double x = 1.0;
+                bool nan = false;
+                if (fabs(num) < 1.0) x = num;
+                else if (num >= 1.0) x = 1.0;
+                else if (num <= -1.0) x = -1.0;
+                else { log_err(R, 44); nan = true; }
+                // (phi_old - phi_det) mod 2 pi in [0, pi): its sine > 0, or the azimuths equal
+                const double sd = spo * R.cdphi - cpo * R.sdphi, cd = cpo * R.cdphi + spo * R.sdphi;
+                const bool flip = sd > 0.0 || (sd == 0.0 && cd > 0.0);
+                const double c2p = fma(2.0 * x, x, -1.0);
+                double s2p = dsqrt(1.0 - c2p * c2p);
+                if (flip ? (x > 0.0 && !nan) : (x < 0.0)) s2p = -s2p;
                 if (fabs(mu) < 1.0) {
-                    polarization_rotation(R, mu, phs, st, sc, dz, R.det2, so, true);
+                    polarization_rotation_cs(R, mu, c2p, s2p, !flip, flip && !nan, st, sc, dz, R.det2, so, true);
                     have_out = true;
                 } else {
                     log_err(R, 49);
@@ -665,12 +675,14 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         c_scat++;
         if (R.rec) S.d[slot].nscat += 1;
         Rng rng; rng.s0 = L0.r0; rng.s1 = L0.r1;
-        double alpha, beta, c2b, s2b;
-        sample_angles<TC::CS>(G, R, G.cums + (size_t)mid * TC::CUM, rng, st, alpha, beta, c2b, s2b);
+        double alpha, beta, c2b, s2b, adeg;
+        sample_angles<TC::CS>(G, R, G.cums + (size_t)mid * TC::CUM, rng, st, alpha, beta, c2b, s2b, &adeg);
         double e0, e1, e2;
-        direction_cosine<true>(R, alpha, beta, dx, dy, dz, e0, e1, e2, phi_old);
+        direction_cosine_cs(R, alpha, beta, dx, dy, dz, cpo, spo, e0, e1, e2);
+        // the matrix at the sampled angle itself (degrees), not at acos(cos(angle)) (ARTES.f90:
+        // 1448-1450): the same bin and fraction to ~1e-14
         double sc[16];
-        interp_matrix<TL::RS, TL::RS4>(P, sym, acos(alpha), sc);
+        interp_matrix_deg<TL::RS, TL::RS4>(P, sym, adeg, sc);
         if (fabs(alpha) < 1.0) {
             double sn[4];
             polarization_rotation<true>(R, alpha, beta, st, sc, dz, e2, sn, false, c2b, s2b);

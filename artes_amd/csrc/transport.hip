@@ -776,6 +776,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.det_phi = atan2(R.det1, R.det0);
     if (R.det_phi < 0.0) R.det_phi += 2.0 * M_PI;
     if (R.det_phi > 2.0 * M_PI) R.det_phi -= 2.0 * M_PI;
+    R.cdphi = cos(R.det_phi); R.sdphi = sin(R.det_phi);
     R.x_max = p->x_max; R.y_max = p->y_max; R.fstop = p->fstop; R.pmin = p->photon_minimum;
     R.surface_albedo = p->surface_albedo; R.theta_star = p->theta_star; R.phi_star = p->phi_star;
     R.det = g->d_copies; R.det_stride = stride;
