@@ -721,6 +721,12 @@ __host__ __device__ inline size_t event_cum_doubles(int nmat) {
 //         HBM copy once at the end.  Float atomics to HBM execute at the memory side and
 //         stay in vmcnt for thousands of cycles, so every later load of the wave waited
 //         for them; the grid is one wave of resident blocks, each looping over many events.
+// line 0 of the next event's record loaded one event ahead (32 VGPRs); ARTES_EV_PREFETCH=0
+// loads it at the event's start (A/B builds)
+#ifndef ARTES_EV_PREFETCH
+#define ARTES_EV_PREFETCH 1
+#endif
+static constexpr bool EV_PREFETCH = ARTES_EV_PREFETCH != 0;
 #ifndef ARTES_EVENT_WPE
 #define ARTES_EVENT_WPE 2
 #endif
@@ -789,11 +795,15 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
     int slot = i < n ? L.event[i] : -1;
     int slot_n = i + stride < n ? L.event[i + stride] : -1;
     Line0 cur;
-    if (slot >= 0) cur = *(const Line0*)(S.s + slot);
+    if (EV_PREFETCH && slot >= 0) cur = *(const Line0*)(S.s + slot);
     for (; i < n_pad; i += stride) {
         const int slot_nn = i + 2 * stride < n ? L.event[i + 2 * stride] : -1;
         Line0 nxt;
-        if (slot_n >= 0) nxt = *(const Line0*)(S.s + slot_n);
+        if constexpr (EV_PREFETCH) {
+            if (slot_n >= 0) nxt = *(const Line0*)(S.s + slot_n);
+        } else {
+            if (slot >= 0) cur = *(const Line0*)(S.s + slot);
+        }
 #ifdef ARTES_DEBUG
         if (i < n) dbg_claim(R, L, slot, S.P, 1, slot >= 0 && to_event_list(cur.mode));
 #endif
@@ -809,7 +819,7 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         wave_append(dest == 2, emit_entry(slot, S_END_DROP), L.emit, L.emit_n);   // (event_one set S_END_DROP)
         slot = slot_n;
         slot_n = slot_nn;
-        cur = nxt;
+        if constexpr (EV_PREFETCH) cur = nxt;
     }
     D.flush_wave();
     if constexpr (LDS_D) {

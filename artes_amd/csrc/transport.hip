@@ -469,6 +469,13 @@ static void dump_live(artes_grid* g, const int* cnt, int in, hipStream_t stream)
     }
 }
 
+// k_event's large block: one block per CU sharing one LDS copy of the tables;
+// 768 threads = 3 waves per SIMD at <= 170 VGPRs (ARTES_EVB=1024 builds the 4-wave variant, <= 128)
+#ifndef ARTES_EVB
+#define ARTES_EVB 768
+#endif
+constexpr int EVB = ARTES_EVB;
+
 template <bool G3D>
 static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R, bool trace, hipStream_t stream) {
     int32_t rc = ensure_pool(g, R.n);
@@ -499,47 +506,47 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     // (k_event PIX1) instead of same-address atomics; ARTES_PIX1=0 turns it off
     const char* p1 = getenv("ARTES_PIX1");
     const bool pix1 = (p1 ? atoi(p1) != 0 : true) && R.nx == 1 && R.ny == 1;
-    // k_event's block with both the tables and the detector in LDS: 768 threads, one block
+    // k_event's block with both the tables and the detector in LDS: EVB threads, one block
     // (12 waves, 3 per SIMD at <= 170 VGPRs) per CU sharing one LDS copy, instead of two
     // 256-thread blocks (2 waves per SIMD, LDS-bound): k_event -7 % on ray3d / hg / iso
     // (ARTES_EVENT_BLOCK=256 for the old shape)
     const char* ebs = getenv("ARTES_EVENT_BLOCK");
-    const int ev_block = ebs && atoi(ebs) == 256 ? 256 : 768;
+    const int ev_block = ebs && atoi(ebs) == 256 ? 256 : EVB;
     // matrices too many for LDS: their cumulative tables alone in LDS (k_event LDS_C) when
-    // they fit beside the detector or the one-pixel lane slots in one 768-thread block per
+    // they fit beside the detector or the one-pixel lane slots in one EVB-thread block per
     // CU; ARTES_EVENT_LDSC=0 turns it off
     const char* elc = getenv("ARTES_EVENT_LDSC");
     const size_t cum_bytes = event_cum_doubles(G.nmat) * sizeof(double);
-    const bool ev_ldsc_ok = !ev_lds && ev_block == 768 && (elc ? atoi(elc) != 0 : true);
+    const bool ev_ldsc_ok = !ev_lds && ev_block == EVB && (elc ? atoi(elc) != 0 : true);
     const char* dl = getenv("ARTES_DET_LDS");
     const bool det_lds = !pix1 && (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
     const size_t lds_cap = 160 * 1024 - 4096;   // (a margin for static LDS)
-    const bool ev_ldsc = ev_ldsc_ok && cum_bytes + (pix1 ? pix1_slot_bytes(768) : det_lds ? det_bytes : 0) <= lds_cap;
+    const bool ev_ldsc = ev_ldsc_ok && cum_bytes + (pix1 ? pix1_slot_bytes(EVB) : det_lds ? det_bytes : 0) <= lds_cap;
     const size_t tab_bytes = ev_lds ? ev_bytes : (ev_ldsc ? cum_bytes : 0);
     int ev_blocks = side_blocks;
     if (det_lds) {
         const size_t b = tab_bytes + det_bytes;
-        int per_cu = ev_block == 768 ? (ev_lds ? blocks_per_cu(g, k_event<true, true, false, 768>, b, 768)
-                                               : ev_ldsc ? blocks_per_cu(g, k_event<false, true, false, 768, true>, b, 768)
-                                                         : blocks_per_cu(g, k_event<false, true, false, 768>, b, 768))
+        int per_cu = ev_block == EVB ? (ev_lds ? blocks_per_cu(g, k_event<true, true, false, EVB>, b, EVB)
+                                               : ev_ldsc ? blocks_per_cu(g, k_event<false, true, false, EVB, true>, b, EVB)
+                                                         : blocks_per_cu(g, k_event<false, true, false, EVB>, b, EVB))
                                      : (ev_lds ? blocks_per_cu(g, k_event<true, true>, b) : blocks_per_cu(g, k_event<false, true>, b));
         const char* eb = getenv("ARTES_EVENT_BPC");
         if (eb) per_cu = std::max(1, atoi(eb));
         ev_blocks = round_sub(per_cu * g->num_cus);
     }
-    // the one-pixel kernel in 768-thread blocks too: the launch bound holds it to 3 waves per
+    // the one-pixel kernel in EVB-thread blocks too: the launch bound holds it to 3 waves per
     // SIMD (<= 168 VGPRs; 211-219 at 256 threads, i.e. 2 waves)
-    const bool pix1_768 = pix1 && ev_block == 768;
-    const size_t p1_bytes = tab_bytes + pix1_slot_bytes(pix1_768 ? 768 : BLOCK);
-    if (pix1_768) {
-        const int per_cu = ev_lds ? blocks_per_cu(g, k_event<true, false, true, 768>, p1_bytes, 768)
-                                  : ev_ldsc ? blocks_per_cu(g, k_event<false, false, true, 768, true>, p1_bytes, 768)
-                                            : blocks_per_cu(g, k_event<false, false, true, 768>, p1_bytes, 768);
+    const bool pix1_big = pix1 && ev_block == EVB;
+    const size_t p1_bytes = tab_bytes + pix1_slot_bytes(pix1_big ? EVB : BLOCK);
+    if (pix1_big) {
+        const int per_cu = ev_lds ? blocks_per_cu(g, k_event<true, false, true, EVB>, p1_bytes, EVB)
+                                  : ev_ldsc ? blocks_per_cu(g, k_event<false, false, true, EVB, true>, p1_bytes, EVB)
+                                            : blocks_per_cu(g, k_event<false, false, true, EVB>, p1_bytes, EVB);
         ev_blocks = round_sub(per_cu * g->num_cus);
     }
-    // the global-detector kernel with LDS_C: one 768-thread block per CU as well
+    // the global-detector kernel with LDS_C: one EVB-thread block per CU as well
     const bool glob_ldsc = ev_ldsc && !pix1 && !det_lds;
-    if (glob_ldsc) ev_blocks = round_sub(blocks_per_cu(g, k_event<false, false, false, 768, true>, cum_bytes, 768) * g->num_cus);
+    if (glob_ldsc) ev_blocks = round_sub(blocks_per_cu(g, k_event<false, false, false, EVB, true>, cum_bytes, EVB) * g->num_cus);
     // the packet ids of the call split into NSUB contiguous ranges, one per sub-engine
     const uint64_t chunk = (R.n + NSUB - 1) / NSUB;
     uint64_t sub_first[NSUB], sub_n[NSUB];
@@ -591,17 +598,17 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         SubLists L = lists(in);
         launch_trace_any<G3D>(g, wpe, trace_bpc, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
-            if (pix1_768 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true, 768>), dim3(ev_blocks), dim3(768), p1_bytes, stream, G, R, g->pool, L);
-            else if (pix1_768 && ev_ldsc) hipLaunchKernelGGL((k_event<false, false, true, 768, true>), dim3(ev_blocks), dim3(768), p1_bytes, stream, G, R, g->pool, L);
-            else if (det_lds && ev_ldsc) hipLaunchKernelGGL((k_event<false, true, false, 768, true>), dim3(ev_blocks), dim3(768), cum_bytes + det_bytes, stream, G, R, g->pool, L);
-            else if (glob_ldsc) hipLaunchKernelGGL((k_event<false, false, false, 768, true>), dim3(ev_blocks), dim3(768), cum_bytes, stream, G, R, g->pool, L);
-            else if (pix1_768) hipLaunchKernelGGL((k_event<false, false, true, 768>), dim3(ev_blocks), dim3(768), p1_bytes, stream, G, R, g->pool, L);
+            if (pix1_big && ev_lds) hipLaunchKernelGGL((k_event<true, false, true, EVB>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L);
+            else if (pix1_big && ev_ldsc) hipLaunchKernelGGL((k_event<false, false, true, EVB, true>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L);
+            else if (det_lds && ev_ldsc) hipLaunchKernelGGL((k_event<false, true, false, EVB, true>), dim3(ev_blocks), dim3(EVB), cum_bytes + det_bytes, stream, G, R, g->pool, L);
+            else if (glob_ldsc) hipLaunchKernelGGL((k_event<false, false, false, EVB, true>), dim3(ev_blocks), dim3(EVB), cum_bytes, stream, G, R, g->pool, L);
+            else if (pix1_big) hipLaunchKernelGGL((k_event<false, false, true, EVB>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L);
             else if (pix1 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L);
             else if (pix1) hipLaunchKernelGGL((k_event<false, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L);
-            else if (ev_lds && det_lds && ev_block == 768) hipLaunchKernelGGL((k_event<true, true, false, 768>), dim3(ev_blocks), dim3(768), ev_bytes + det_bytes, stream, G, R, g->pool, L);
+            else if (ev_lds && det_lds && ev_block == EVB) hipLaunchKernelGGL((k_event<true, true, false, EVB>), dim3(ev_blocks), dim3(EVB), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
             else if (ev_lds) hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
-            else if (det_lds && ev_block == 768) hipLaunchKernelGGL((k_event<false, true, false, 768>), dim3(ev_blocks), dim3(768), det_bytes, stream, G, R, g->pool, L);
+            else if (det_lds && ev_block == EVB) hipLaunchKernelGGL((k_event<false, true, false, EVB>), dim3(ev_blocks), dim3(EVB), det_bytes, stream, G, R, g->pool, L);
             else if (det_lds) hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L);
             else hipLaunchKernelGGL((k_event<false, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
         });
