@@ -749,7 +749,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     const bool grid3d = (T.ntheta > 1 || T.nphi > 1);
     // (coarse 3D grids -- the cloudy atmospheres of configs[3], ~600 cells -- have short traces
     // and refill best at 32: cloudy phase +2.7 %, spectrum +4 %, profiles/r03/cloudy_ldsc_refill.txt)
-    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? (T.ncell < 4096 ? 32 : 16) : 20);
+    // (round 4, with the trace-relative radial family: radial-only grids 28 -- hg +2 %, iso +14 %
+    // against 20 -- and coarse 3D grids 28 -- the cloudy calls +1.5 % against 32; fine 3D grids
+    // stay at 16; profiles/r04/ab/refill_after_trel.txt)
+    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? (T.ncell < 4096 ? 28 : 16) : 28);
     // ended chains' list appends at the wave's next refill (kernel_trace.hpp `append`): ray3d
     // +3.7 %, hg +5.1 %, iso +2.7 %, the cloudy configs[3] calls +3.4-3.8 % (3e8 / 1e8 packets,
     // profiles/r03/late_append_ab.txt)
@@ -771,6 +774,11 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // radial-only ones; profiles/r02/refill_hbatch_sweep*.txt)
     const char* hb = getenv("ARTES_HBATCH");
     R.hbatch = hb ? std::max(1, std::min(64, atoi(hb))) : (grid3d ? 6 : 4);
+    // trace-relative kernels: a lane whose nearest entry is a theta / phi bound waits until
+    // this many lanes of the wave need that evaluation (or few lanes still step), so the
+    // wave runs the theta / phi form in fewer iterations
+    const char* gb = getenv("ARTES_GBATCH");
+    R.gbatch = gb ? std::max(1, std::min(64, atoi(gb))) : 4;
     // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
     // 48 on 3D grids, 40 on radial-only ones (re-swept with the sub-engines: hg best at
     // 32-40, iso flat from 40 to 64; tools/static_sweep.sh)

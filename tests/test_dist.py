@@ -82,3 +82,24 @@ def test_two_rank_gloo_equals_single_process(tmp_path):
     # the flow diagnostics are summed over the ranks too
     np.testing.assert_allclose(np.load(out.replace(".npy", "_flow.npy")), fg1, rtol=1e-10, atol=1e-12 * np.abs(fg1).max())
     np.testing.assert_allclose(np.load(out.replace(".npy", "_lat.npy")), ft1, rtol=1e-11, atol=1e-300)
+
+
+def test_device_of_is_local_rank_modulo_visible_devices(monkeypatch):
+    """One rank-to-device rule for the CLI, the bench and the RCCL device (dist.device_of):
+    local_rank modulo the visible devices, so ranks sharing one card (the gloo rehearsal on a
+    one-GPU box) and launchers that show each rank one GPU both map inside [0, count)."""
+    import torch
+
+    for count, local, want in ((8, 3, 3), (1, 1, 0), (1, 7, 0), (0, 5, 0), (2, 5, 1)):
+        monkeypatch.setattr(torch.cuda, "device_count", lambda c=count: c)
+        assert dist.device_of(dist.Rank(rank=local, world=8, local_rank=local)) == want
+
+
+def test_bench_host_cores_reports_the_usable_count():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    c = bench.host_cores()
+    assert c["affinity"] == len(os.sched_getaffinity(0)) and 1 <= c["usable"] <= c["affinity"] <= c["visible"]

@@ -39,6 +39,8 @@ for name in (os.environ.get("LS_WORKLOAD", "ray3d"),):
         nretry, nsetup = int(r.err[4]), int(r.err[5])
         firuns, filanes, reflanes = int(r.err[6]), int(r.err[7]), int(r.err[8])
         hruns, hlanes = int(r.err[9]), int(r.err[10])
+        f12, anyf12 = int(r.err[17]), int(r.err[22])
+        f2, anyf2 = int(r.err[23]), int(r.err[24])
         print(f"{name} {env}: {g.last_kernel_ms():.1f} ms ({n / g.last_kernel_ms() / 1e3:.1f} Mpkt/s) trace {kt['trace'][0]:.1f} ms, "
               f"wave-steps {steps:.3e}, lanes/step {lanes / steps:.1f}, crossings/wave-step {C / steps:.1f}, "
               f"steps/refill {steps / max(refills, 1):.1f}, tail steps {tsteps / steps:.3f} at {tlanes / max(tsteps, 1):.1f} lanes, "
@@ -46,7 +48,9 @@ for name in (os.environ.get("LS_WORKLOAD", "ray3d"),):
               f"moving lanes/iteration {nmove / steps:.1f}, other-face retries {nretry / steps:.2f}, evaluations without a step {nsetup / steps:.2f}, "
               f"first-interaction block in {firuns / steps:.3f} of iterations ({filanes / max(firuns, 1):.2f} lanes), "
               f"lanes refilled per refill {reflanes / max(refills, 1):.1f}, "
-              f"interaction block in {hruns / steps:.3f} of iterations ({hlanes / max(hruns, 1):.2f} lanes)",
+              f"interaction block in {hruns / steps:.3f} of iterations ({hlanes / max(hruns, 1):.2f} lanes), "
+              f"theta / phi evaluations {f12 / steps:.2f} lanes per wave-step, in {anyf12 / steps:.3f} of iterations "
+              f"(phi: {f2 / steps:.2f} lanes, in {anyf2 / steps:.3f})",
               flush=True)
         for k, v in old.items():
             if v is None:
