@@ -442,13 +442,13 @@ __device__ __forceinline__ double radial_tr(const TraceTabs& T, double b0, doubl
     const double dA = sA - t, dB = sB - t;
     const bool same = onr & (fi == cr + (ch ? 1 : 0));
     const double tmin = (same & ch) ? K.tol_same : K.tol;
-    const bool ok = (disc >= 0.0) & !(same & !ch);
-    bool vA = ok & (dA > tmin), vB = ok & (dB > tmin);
-    const bool eq = vA & vB & (dA == dB);
-    vA = vA & !eq & (dA < K.huge);
-    vB = vB & !eq & (dB < K.huge);
+    // (equal roots give none: with dA == dB both pass or fail their tests together, so the
+    // rule is one more term of each AND chain; the chains stay lane masks, and the nearer
+    // valid root is one min -- sA <= sB -- instead of a branch)
+    const bool ok = (disc >= 0.0) & !(same & !ch) & (dA != dB);
+    const bool vA = ok & (dA > tmin) & (dA < K.huge), vB = ok & (dB > tmin) & (dB < K.huge);
     outer = ch;
-    return vA ? sA : or_nan(vB, sB);
+    return min_nonan(or_nan(vA, sA), or_nan(vB, sB));
 }
 
 // ---------------------------------------------- phi family, trace-relative (TREL) ---
