@@ -42,8 +42,18 @@ static constexpr bool TREL_PHI = false;  // A/B builds: phi in the batched per-s
 #else
 static constexpr bool TREL_PHI = true;   // the phi family trace-relative too (phi_tr), outside the batched theta form
 #endif
+// ARTES_DEBUG_TIMING (development build, tools/time_regions.py): per wave, the shader-clock
+// cycles spent in each region of the k_trace loop, summed into the error slots 0-7 (the
+// run's error codes are void then)
+#ifdef ARTES_DEBUG_TIMING
+#define TM_TICK(v) const unsigned long long v = tm_tick()
+#define TM_ADD(k, d) tm_add(k, d)
+#else
+#define TM_TICK(v)
+#define TM_ADD(k, d)
+#endif
 #ifdef ARTES_LOOKAHEAD
-static constexpr bool LOOKAHEAD = true;    // A/B builds: slot ids from the chunk registers, records prefetched (kernel_event.hpp)
+static constexpr bool LOOKAHEAD = true;   // A/B builds: slot ids from the chunk registers, records prefetched (kernel_event.hpp)
 #else
 static constexpr bool LOOKAHEAD = false;   // refills load list entries and records on demand ("lookahead refills")
 #endif
@@ -546,6 +556,22 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 
         }
     }
+#ifdef ARTES_DEBUG_TIMING
+    __shared__ unsigned long long s_tm[BLOCK / 64][8];
+    unsigned long long* const my_tm = s_tm[threadIdx.x >> 6];
+    if ((threadIdx.x & 63) < 8) my_tm[threadIdx.x & 63] = 0;
+    __builtin_amdgcn_wave_barrier();
+    auto tm_tick = [&]() -> unsigned long long {
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long t = __builtin_readcyclecounter();
+        __builtin_amdgcn_sched_barrier(0);
+        return t;
+    };
+    auto tm_add = [&](int k, unsigned long long d) {   // by the wave's first active lane
+        if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) my_tm[k] += d;
+    };
+    TM_TICK(t_begin);
+#endif
     const int fam_all = !G3D ? 1 : (G.nphi > 1 ? 7 : 3);
     const int nrt = G.nr * G.ntheta;        // linear-index stride of phi
     bool have = false;
@@ -814,6 +840,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             break;
         }
         int end = 0;   // 0: continue, else the slot's new mode
+        TM_TICK(t0);
         {
             const unsigned long long pk = __ballot(parked != 0);
             if (pk) {
@@ -844,6 +871,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }
         }
+        TM_TICK(t1);
+        TM_ADD(0, t1 - t0);
         // ---------------------------------------------------------------- refill
         if (!exhausted) {
             const unsigned long long idle = __ballot(!have);
@@ -893,6 +922,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }
         }
+        TM_TICK(t2);
+        TM_ADD(1, t2 - t1);
         if (!__any(have) && exhausted) break;   // (all lanes idle otherwise: every grab was a hole)
 #ifdef ARTES_DEBUG_LANES
         dbg_steps++;
@@ -950,10 +981,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     } else if (TREL_PHI && fam == 2) {
                         dm = phi_tr(T, tx, ty, nx, ny, tpar, tft, tfi, tcp, pout, K, outer);
                     } else {   // theta / phi (~0.1-0.4 % of crossings): from the current point
+                        TM_TICK(ta);
                         const double qx = fma(tpar, nx, tx), qy = fma(tpar, ny, ty), qz = fma(tpar, nz, tz);
                         dm = tpar + family_eval1<G3D, OBL, true>(G, T, fam, qx, qy, qz, nx, ny, nz, dir_axy(ax2, by2, nx, ny),
                                                                  cz2 * nz * nz, tft, tfi, tcr, tct, tcp, pout, -qz * fast_rcp(nz), alt, K,
                                                                  outer);
+                        TM_TICK(tb);
+                        TM_ADD(5, tb - ta);
                     }
                 } else {
                     dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
@@ -1004,6 +1038,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             }
 #endif
             }   // run_eval
+            TM_TICK(tev);
+            TM_ADD(2, tev - t2);
             // ---------------------------------------------------- trace step
             // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
             // The nearest distance of the three is the reference's choice whenever it
@@ -1163,6 +1199,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }   // pending == 0
         }   // have
+        TM_TICK(t3);
+        TM_ADD(3, t3 - t2);
         if (end) {   // the chain ends: the record now, the list append below or at the next refill
             c_cross += (uint32_t)(ncross - nc0);
             Slot* rec = S.s + slot;
@@ -1179,6 +1217,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         if (!R.late_append) append();
         q_event.flush_if(QFLUSH, L.event, L.event_n);
         q_emit.flush_if(QFLUSH, L.emit, L.emit_n);
+        TM_TICK(t4);
+        TM_ADD(4, t4 - t3);
+        TM_ADD(6, 1);
 #ifdef ARTES_DEBUG_LANES
         {
             const unsigned long long bs = __ballot(dbg_s), bh = __ballot(dbg_h), bm = __ballot(dbg_m);
@@ -1191,6 +1232,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     q_event.flush(L.event, L.event_n);
     q_emit.flush(L.emit, L.emit_n);
     if constexpr (LOOKAHEAD) prefetch_drain();
+#ifdef ARTES_DEBUG_TIMING
+    {
+        TM_TICK(t_end);
+        TM_ADD(7, t_end - t_begin);
+        __builtin_amdgcn_wave_barrier();
+        if ((threadIdx.x & 63) < 8) atomicAdd(&R.err[threadIdx.x & 63], my_tm[threadIdx.x & 63]);
+    }
+#endif
 #ifdef ARTES_DEBUG_LANES
     if ((threadIdx.x & 63) == 0) {
         // (development build: error slots reused as counters, the run's error codes are void)
