@@ -557,9 +557,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         }
     }
 #ifdef ARTES_DEBUG_TIMING
-    __shared__ unsigned long long s_tm[BLOCK / 64][8];
+    __shared__ unsigned long long s_tm[BLOCK / 64][16];
     unsigned long long* const my_tm = s_tm[threadIdx.x >> 6];
-    if ((threadIdx.x & 63) < 8) my_tm[threadIdx.x & 63] = 0;
+    if ((threadIdx.x & 63) < 16) my_tm[threadIdx.x & 63] = 0;
     __builtin_amdgcn_wave_barrier();
     auto tm_tick = [&]() -> unsigned long long {
         __builtin_amdgcn_sched_barrier(0);
@@ -854,20 +854,26 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     dbg_firuns++;
                     dbg_filanes += __popcll(pf);
 #endif
+                    TM_TICK(tf0);
                     if (parked & 1) {
                         first_interaction(parked & 2);
                         parked = 0;
                     }
+                    TM_TICK(tf1);
+                    TM_ADD(13, tf1 - tf0);
                 }
                 if (ph && (__popcll(ph) >= R.hbatch || force)) {
 #ifdef ARTES_DEBUG_LANES
                     dbg_hruns++;
                     dbg_hlanes += __popcll(ph);
 #endif
+                    TM_TICK(th0);
                     if (parked == 4) {
                         end = interaction();
                         parked = 0;
                     }
+                    TM_TICK(th1);
+                    TM_ADD(14, th1 - th0);
                 }
             }
         }
@@ -878,16 +884,29 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             const unsigned long long idle = __ballot(!have);
             if (__popcll(idle) >= R.refill || idle == __ballot(true)) {
                 append();
+                TM_TICK(tr_a);
+                TM_ADD(8, tr_a - t1);
                 TraceCursor cur = load_cursor(my_cur);
                 int my;
                 if constexpr (LOOKAHEAD) {
                     int sl;
-                    my = wave_take<true>(cur, L.grab, home, !have, &sl, &ck_cur, &ck_nxt, &L, split, S.s, pf_sink);
+                    my = wave_take<true>(cur, L.grab, home, !have, R.dgrab, &sl, &ck_cur, &ck_nxt, &L, split, S.s, pf_sink);
                     if (!have && my >= 0) slot = sl != -2 ? sl : L.trace_in[list_pos(my, split, L.P)];
                 } else {
-                    my = wave_take(cur, L.grab, home, !have);
+                    my = wave_take(cur, L.grab, home, !have, R.dgrab);
+                    TM_TICK(tr_b);
+                    TM_ADD(9, tr_b - tr_a);
                     if (!have && my >= 0) slot = L.trace_in[list_pos(my, split, L.P)];
+#ifdef ARTES_DEBUG_TIMING
+                    asm volatile("" ::"v"(slot));   // (the list entry's wait inside this region)
+                    my_tm[15] = tm_tick() - tr_b;   // (lane-0 scratch: added below)
+#endif
                 }
+                TM_TICK(tr_c);
+#ifdef ARTES_DEBUG_TIMING
+                __builtin_amdgcn_wave_barrier();
+                if (!LOOKAHEAD) TM_ADD(10, my_tm[15]);
+#endif
                 if ((threadIdx.x & 63) == 0) *my_cur = cur;
                 __builtin_amdgcn_wave_barrier();
                 exhausted = cur.exhausted;
@@ -904,6 +923,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
                 dbg_reflanes += __popcll(__ballot(!have && my >= 0 && slot >= 0));
 #endif
+#ifdef ARTES_DEBUG_TIMING
+                unsigned long long tr_d = tm_tick();
+                bool did = false;
+#endif
                 if (!have && my >= 0 && slot >= 0) {   // -1: a hole left by a dropped or retired packet
                     const Slot* rec = S.s + slot;
                     mode = rec->mode;
@@ -915,11 +938,31 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     ncross = rec->ncross;
                     nc0 = ncross;
                     wI = rec->wI;
+#ifdef ARTES_DEBUG_TIMING
+                    asm volatile("" ::"v"(px), "v"(wI), "v"(ncross), "v"(ldz));   // (the record's wait before the set-up)
+                    tr_d = tm_tick();
+                    did = true;
+#endif
                     const bool peel = is_peel_trace(mode);
                     start_trace(peel ? R.det0 : ldx, peel ? R.det1 : ldy, peel ? R.det2 : ldz);
                     have = true;
                     kb = (mode == S_FIRST) ? ncross : 0;
                 }
+#ifdef ARTES_DEBUG_TIMING
+                {   // record loads / set-up split at the first refilling lane's clock
+                    TM_TICK(tr_e);
+                    const unsigned long long rb = __ballot(did);
+                    if (rb) {
+                        const int fl = __builtin_ctzll(rb);
+                        const unsigned long long td = ((unsigned long long)(unsigned)__shfl((int)(tr_d >> 32), fl) << 32) |
+                                                      (unsigned)__shfl((int)tr_d, fl);
+                        TM_ADD(11, td - tr_c);
+                        TM_ADD(12, tr_e - td);
+                    } else {
+                        TM_ADD(11, tr_e - tr_c);
+                    }
+                }
+#endif
             }
         }
         TM_TICK(t2);
@@ -1237,7 +1280,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         TM_TICK(t_end);
         TM_ADD(7, t_end - t_begin);
         __builtin_amdgcn_wave_barrier();
-        if ((threadIdx.x & 63) < 8) atomicAdd(&R.err[threadIdx.x & 63], my_tm[threadIdx.x & 63]);
+        if ((threadIdx.x & 63) < 16) atomicAdd(&R.err[threadIdx.x & 63], my_tm[threadIdx.x & 63]);
     }
 #endif
 #ifdef ARTES_DEBUG_LANES

@@ -779,11 +779,15 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // wave runs the theta / phi form in fewer iterations
     const char* gb = getenv("ARTES_GBATCH");
     R.gbatch = gb ? std::max(1, std::min(64, atoi(gb))) : 4;
+    // the least list entries a dynamic grab of k_trace asks for (the wave keeps the rest for
+    // its next refills; kernel_event.hpp, wave_take): 128 (profiles/r04/ab/dyn_grab_sweep*.txt)
+    const char* dg = getenv("ARTES_DGRAB");
+    R.dgrab = dg ? std::max(1, std::min(4096, atoi(dg))) : 128;
     // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
-    // 48 on 3D grids, 40 on radial-only ones (re-swept with the sub-engines: hg best at
-    // 32-40, iso flat from 40 to 64; tools/static_sweep.sh)
+    // 32 on 3D grids, 24 on radial-only ones since the dynamic grabs ask for 128 entries
+    // (48 / 40 before: each grab was an atomic round trip; profiles/r04/ab/dyn_grab_sweep2_static.txt)
     const char* sq = getenv("ARTES_STATIC");
-    R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : (grid3d ? 48 : 40);
+    R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : (grid3d ? 32 : 24);
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)
     R.det1 = sin(p->det_theta) * sin(p->det_phi);
     R.det2 = cos(p->det_theta);

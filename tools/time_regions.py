@@ -36,7 +36,7 @@ for env in variants:
     g.kernel_times()
     r = g.run(p, 0, n, 2024)
     kt = g.kernel_times()
-    e = [int(r.err[k]) for k in range(8)]
+    e = [int(r.err[k]) for k in range(16)]
     total, iters = e[7], max(e[6], 1)
     C = r.counter("crossings")
     print(f"{name} {env}: {g.last_kernel_ms():.1f} ms, k_trace {kt['trace'][0]:.1f} ms, wave-iterations {iters:.3e}, "
@@ -46,7 +46,12 @@ for env in variants:
         print(f"    {lab:62s} {v / total:6.3f}  ({v / iters:7.0f} cycles per iteration)")
     rest = total - sum(split)
     print(f"    {'outside the loop regions (loop head, exit, staging)':62s} {rest / total:6.3f}")
-    print(f"    {'  of the evaluation: the batched theta form':62s} {e[5] / total:6.3f}  ({e[5] / iters:7.0f} cycles per iteration)")
+    subs = [("  of the parked blocks: the first interaction", e[13]), ("  of the parked blocks: interaction + peel set-up", e[14]),
+            ("  of the refill: append (late list appends)", e[8]), ("  of the refill: take (cursor, chunk grabs)", e[9]),
+            ("  of the refill: list entry load", e[10]), ("  of the refill: record load", e[11]),
+            ("  of the refill: trace set-up", e[12]), ("  of the evaluation: the batched theta form", e[5])]
+    for lab, v in subs:
+        print(f"    {lab:62s} {v / total:6.3f}  ({v / iters:7.0f} cycles per iteration)")
     for k, v in old.items():
         if v is None:
             os.environ.pop(k, None)
