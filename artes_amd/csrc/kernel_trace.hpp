@@ -42,6 +42,9 @@ static constexpr bool TREL_PHI = false;  // A/B builds: phi in the batched per-s
 #else
 static constexpr bool TREL_PHI = true;   // the phi family trace-relative too (phi_tr), outside the batched theta form
 #endif
+#ifndef ARTES_NREP
+#define ARTES_NREP 1
+#endif
 // ARTES_DEBUG_TIMING (development build, tools/time_regions.py): per wave, the shader-clock
 // cycles spent in each region of the k_trace loop, summed into the error slots 0-7 (the
 // run's error codes are void then)
@@ -976,6 +979,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
         bool dbg_s = false, dbg_h = false, dbg_m = false, dbg_r = false, dbg_u = false;
 #endif
+        // (ARTES_NREP > 1, development builds: the evaluation and step repeated in one iteration,
+        // so the iteration's checks, refill and chain-end blocks run once per NREP steps)
+#pragma unroll
+        for (int rep = 0; rep < ARTES_NREP; rep++) {
         if (have && !parked && !end) {
             const double k = kext;
             // ------------------------------------------- evaluate one face family
@@ -1242,6 +1249,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }   // pending == 0
         }   // have
+        }   // rep
         TM_TICK(t3);
         TM_ADD(3, t3 - t2);
         if (end) {   // the chain ends: the record now, the list append below or at the next refill
