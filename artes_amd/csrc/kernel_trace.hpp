@@ -43,8 +43,9 @@ static constexpr bool TREL_PHI = false;  // A/B builds: phi in the batched per-s
 static constexpr bool TREL_PHI = true;   // the phi family trace-relative too (phi_tr), outside the batched theta form
 #endif
 #ifndef ARTES_NREP
-#define ARTES_NREP 1
+#define ARTES_NREP 8
 #endif
+static constexpr int NREP = ARTES_NREP;   // k_trace: the most steps per loop iteration (unrolled copies)
 // ARTES_DEBUG_TIMING (development build, tools/time_regions.py): per wave, the shader-clock
 // cycles spent in each region of the k_trace loop, summed into the error slots 0-7 (the
 // run's error codes are void then)
@@ -651,11 +652,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     constexpr bool TREL = (LAZY || (!G3D && !OBL && !TWOFACE && !FLOW)) && TREL_ON;
 #endif
     double tpar = 0.0, b0 = 0.0, pm = 0.0;
+#ifdef ARTES_NBF
     const double inv2rtop = LAZY ? 0.5 / sqrt(G.rf2[G.nr]) : 0.0;
+#endif
     auto set_bounds = [&]() {
         if constexpr (LAZY) {
+#ifdef ARTES_NBF
             const double r2 = fma(tx, tx, fma(ty, ty, tz * tz));
             const double br = min_nonan(T.fr[tcr + 1].off - r2, r2 - T.fr[tcr].off) * inv2rtop;
+#else
+            // (the radial family is the lowest pending bit, so a new trace evaluates it in its
+            // first iteration, before any step reads e0: its bound would never be read)
+            const double br = 0.0;
+#endif
             const double rho = fast_sqrt(fma(tx, tx, ty * ty));
             const double2 c0 = T.tcs[tct], c1 = T.tcs[tct + 1];
             const double bt = min_nonan(min_nonan(fabs(fma(rho, c0.x, -tz * c0.y)), fabs(fma(rho, c0.x, tz * c0.y))),
@@ -979,10 +988,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
         bool dbg_s = false, dbg_h = false, dbg_m = false, dbg_r = false, dbg_u = false;
 #endif
-        // (ARTES_NREP > 1, development builds: the evaluation and step repeated in one iteration,
-        // so the iteration's checks, refill and chain-end blocks run once per NREP steps)
+        // The evaluation and the step, R.nrep times per iteration (unrolled, at most NREP): the
+        // iteration's wave-level blocks -- parked-lane ballots and blocks, refill check and
+        // refill, chain-end stores, queue flushes, loop head -- run once per R.nrep steps.  A
+        // lane that ends, parks or waits for a theta batch sits out the rest of the iteration
+        // ("Several steps per iteration").
 #pragma unroll
-        for (int rep = 0; rep < ARTES_NREP; rep++) {
+        for (int rep = 0; rep < NREP; rep++) {
         if (have && !parked && !end) {
             const double k = kext;
             // ------------------------------------------- evaluate one face family
@@ -1249,6 +1261,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }   // pending == 0
         }   // have
+#ifndef ARTES_FIXED_STEPS
+        if (rep + 1 >= R.nrep) break;   // (wave-uniform: the grid's step count, <= NREP)
+#endif
         }   // rep
         TM_TICK(t3);
         TM_ADD(3, t3 - t2);

@@ -781,6 +781,11 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.gbatch = gb ? std::max(1, std::min(64, atoi(gb))) : 4;
     // the least list entries a dynamic grab of k_trace asks for (the wave keeps the rest for
     // its next refills; kernel_event.hpp, wave_take): 128 (profiles/r04/ab/dyn_grab_sweep*.txt)
+    // k_trace steps per loop iteration: 8 (the build's most, NREP) on fine 3D and radial-only
+    // grids, 4 on coarse 3D grids, whose short chains leave more lanes idle for the rest of an
+    // iteration (profiles/r04/ab/trace_nrep*_ab.txt)
+    const char* nrp = getenv("ARTES_STEPS");
+    R.nrep = std::max(1, std::min(NREP, nrp ? atoi(nrp) : (grid3d && T.ncell < 4096 ? 4 : 8)));
     const char* dg = getenv("ARTES_DGRAB");
     R.dgrab = dg ? std::max(1, std::min(4096, atoi(dg))) : 128;
     // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
