@@ -54,7 +54,6 @@ struct DevRun {
     int nx, ny, photon_scattering, phase_far, stellar_direction, defer, refill, static_q64, batch, batch_min, hbatch;
     int late_append;                // k_trace: list appends of ended chains at the wave's next refill (kernel_trace.hpp)
     int gbatch;                     // k_trace (trace-relative): theta / phi evaluations run once this many lanes wait
-    int nrep;                       // k_trace: steps per loop iteration (1..NREP)
     int dgrab;                      // k_trace: the least list entries a dynamic (atomic) grab asks for
     int photon_source, photon_emission;
     int moments;                    // accumulate packet-level moments (slot line 1, planes 12-15, tot2[0..3])

@@ -42,10 +42,6 @@ static constexpr bool TREL_PHI = false;  // A/B builds: phi in the batched per-s
 #else
 static constexpr bool TREL_PHI = true;   // the phi family trace-relative too (phi_tr), outside the batched theta form
 #endif
-#ifndef ARTES_NREP
-#define ARTES_NREP 8
-#endif
-static constexpr int NREP = ARTES_NREP;   // k_trace: the most steps per loop iteration (unrolled copies)
 // ARTES_DEBUG_TIMING (development build, tools/time_regions.py): per wave, the shader-clock
 // cycles spent in each region of the k_trace loop, summed into the error slots 0-7 (the
 // run's error codes are void then)
@@ -524,7 +520,8 @@ __device__ __noinline__ void flow_segment(double* flow_g, double* flow_t, int ce
 // the other two.  The linear cell index is updated with the crossing, not recomputed.
 //
 // FLOW instantiations add the energy-transport diagnostics to propagation segments.
-template <bool G3D, bool OBL, int WPE, bool FLOW = false>
+// NREP: steps per loop iteration (see the loop).
+template <bool G3D, bool OBL, int WPE, bool FLOW = false, int NREP = 8>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G, DevRun R, Pool S, SubLists SL) {
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_tab[];
@@ -988,11 +985,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #ifdef ARTES_DEBUG_LANES
         bool dbg_s = false, dbg_h = false, dbg_m = false, dbg_r = false, dbg_u = false;
 #endif
-        // The evaluation and the step, R.nrep times per iteration (unrolled, at most NREP): the
-        // iteration's wave-level blocks -- parked-lane ballots and blocks, refill check and
-        // refill, chain-end stores, queue flushes, loop head -- run once per R.nrep steps.  A
-        // lane that ends, parks or waits for a theta batch sits out the rest of the iteration
-        // ("Several steps per iteration").
+        // The evaluation and the step, NREP times per iteration (unrolled): the iteration's
+        // wave-level blocks -- parked-lane ballots and blocks, refill check and refill,
+        // chain-end stores, queue flushes, loop head -- run once per NREP steps.  A lane that
+        // ends, parks or waits for a theta batch sits out the rest of the iteration (DESIGN.md
+        // §4, "Several steps per iteration").  (A compile-time count: a runtime one, a scalar
+        // compare per copy, cost ray3d 3 %.)
 #pragma unroll
         for (int rep = 0; rep < NREP; rep++) {
         if (have && !parked && !end) {
@@ -1261,9 +1259,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
             }   // pending == 0
         }   // have
-#ifndef ARTES_FIXED_STEPS
-        if (rep + 1 >= R.nrep) break;   // (wave-uniform: the grid's step count, <= NREP)
-#endif
         }   // rep
         TM_TICK(t3);
         TM_ADD(3, t3 - t2);

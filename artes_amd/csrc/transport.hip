@@ -416,20 +416,21 @@ static int round_sub(int blocks) { return std::max(NSUB, (blocks + NSUB - 1) / N
 // albedo in LDS as well, for grids whose table fits, measured the same as reading them from
 // L2 -- cloudy 210.8 vs 211.1, hg 705 vs 707 Mpackets/s, profiles/r03/klds_ab.txt -- so they
 // stay in global memory.)
-template <bool G3D, bool OBL, int WPE, bool FLOW = false>
+template <bool G3D, bool OBL, int WPE, bool FLOW = false, int NREP = 8>
 static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L, hipStream_t stream) {
     const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
-    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW>, lds);
+    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW, NREP>, lds);
     g->trace_blocks = round_sub(per_cu * g->num_cus);
     timed(g, ARTES_K_TRACE, stream, [&] {
-        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW, NREP>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
 }
 
 // k_trace variant: 3D or radial-only grid, spheroidal (oblate) or spherical planet,
 // occupancy target (waves per SIMD the register budget is sized for)
+// (steps: k_trace's steps per loop iteration, 8 or 4; see trace_steps)
 template <bool G3D>
-static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L,
+static void launch_trace_any(artes_grid* g, int wpe, int steps, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L,
                              hipStream_t stream) {
     const bool oblate = !(G.ax2 == 1.0 && G.by2 == 1.0 && G.cz2 == 1.0 && G.a == 1.0 && G.b == 1.0);
     if (R.flow_g || R.flow_t) {   // diagnostics: one occupancy target only
@@ -438,9 +439,12 @@ static void launch_trace_any(artes_grid* g, int wpe, int bpc, const DevGrid& G, 
     } else if (oblate) {
         if (wpe == 3) launch_trace<G3D, true, 3>(g, bpc, G, R, L, stream);
         else launch_trace<G3D, true, 4>(g, bpc, G, R, L, stream);
+    } else if (wpe == 3) {
+        launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
+    } else if (G3D && steps == 4) {
+        launch_trace<G3D, false, 4, false, 4>(g, bpc, G, R, L, stream);
     } else {
-        if (wpe == 3) launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
-        else launch_trace<G3D, false, 4>(g, bpc, G, R, L, stream);
+        launch_trace<G3D, false, 4>(g, bpc, G, R, L, stream);
     }
 }
 
@@ -492,6 +496,12 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const int wpe = we ? atoi(we) : 4;
     const char* bp = getenv("ARTES_TRACE_BPC");   // k_trace blocks per CU
     const int trace_bpc = bp ? std::max(1, atoi(bp)) : 0;
+    // k_trace steps per loop iteration ("Several steps per iteration"): 8 on fine
+    // 3D and radial-only grids, 4 on coarse 3D grids (< 4096 cells), whose short chains leave
+    // more lanes idle for the rest of an iteration (profiles/r04/ab/trace_nrep*_ab.txt);
+    // ARTES_STEPS=4|8 overrides (3D grids)
+    const char* ts = getenv("ARTES_STEPS");
+    const int trace_steps = ts ? (atoi(ts) == 4 ? 4 : 8) : (G.ncell < 4096 ? 4 : 8);
     if (trace_table_bytes(G.nr, G.ntheta, G.nphi) > 65536) return fail(-22, "face tables exceed the 64 KiB LDS budget of k_trace");
     // scattering tables in LDS for k_event when they fit next to one another (a few
     // distinct matrices: uniform and layered atmospheres); otherwise read from L2
@@ -596,7 +606,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const long long max_it = mi ? atoll(mi) : 2000000LL;
     for (;;) {
         SubLists L = lists(in);
-        launch_trace_any<G3D>(g, wpe, trace_bpc, G, R, L, stream);
+        launch_trace_any<G3D>(g, wpe, trace_steps, trace_bpc, G, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] {
             if (pix1_big && ev_lds) hipLaunchKernelGGL((k_event<true, false, true, EVB>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L);
             else if (pix1_big && ev_ldsc) hipLaunchKernelGGL((k_event<false, false, true, EVB, true>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L);
@@ -781,11 +791,6 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.gbatch = gb ? std::max(1, std::min(64, atoi(gb))) : 4;
     // the least list entries a dynamic grab of k_trace asks for (the wave keeps the rest for
     // its next refills; kernel_event.hpp, wave_take): 128 (profiles/r04/ab/dyn_grab_sweep*.txt)
-    // k_trace steps per loop iteration: 8 (the build's most, NREP) on fine 3D and radial-only
-    // grids, 4 on coarse 3D grids, whose short chains leave more lanes idle for the rest of an
-    // iteration (profiles/r04/ab/trace_nrep*_ab.txt)
-    const char* nrp = getenv("ARTES_STEPS");
-    R.nrep = std::max(1, std::min(NREP, nrp ? atoi(nrp) : (grid3d && T.ncell < 4096 ? 4 : 8)));
     const char* dg = getenv("ARTES_DGRAB");
     R.dgrab = dg ? std::max(1, std::min(4096, atoi(dg))) : 128;
     // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
