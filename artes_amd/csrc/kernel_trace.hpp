@@ -1043,9 +1043,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     } else {   // theta / phi (~0.1-0.4 % of crossings): from the current point
                         TM_TICK(ta);
                         const double qx = fma(tpar, nx, tx), qy = fma(tpar, ny, ty), qz = fma(tpar, nz, tz);
+#ifdef ARTES_THETA2   // (development build: both theta faces at once, no other-face retry)
+                        dm = tpar + family_eval<G3D, OBL>(G, T, fam, qx, qy, qz, nx, ny, nz, dir_axy(ax2, by2, nx, ny),
+                                                          cz2 * nz * nz, tft, tfi, tcr, tct, tcp, pout, -qz * fast_rcp(nz), outer);
+#else
                         dm = tpar + family_eval1<G3D, OBL, true>(G, T, fam, qx, qy, qz, nx, ny, nz, dir_axy(ax2, by2, nx, ny),
                                                                  cz2 * nz * nz, tft, tfi, tcr, tct, tcp, pout, -qz * fast_rcp(nz), alt, K,
                                                                  outer);
+#endif
                         TM_TICK(tb);
                         TM_ADD(5, tb - ta);
                     }
@@ -1053,6 +1058,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
                 }
                 retry = (fam != 2) & !alt & !(dm < K.inf);
+#ifdef ARTES_THETA2
+                if constexpr (TREL) retry = retry & (fam == 0);
+#endif
             }
             // (the other face is still to come: no bound.  Only the high word is cleared: the
             // entry is then 0 or a positive denormal, below any step, so the family stays the
