@@ -762,7 +762,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // (round 4, with the trace-relative radial family: radial-only grids 28 -- hg +2 %, iso +14 %
     // against 20 -- and coarse 3D grids 28 -- the cloudy calls +1.5 % against 32; fine 3D grids
     // stay at 16; profiles/r04/ab/refill_after_trel.txt)
-    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? (T.ncell < 4096 ? 28 : 16) : 28);
+    // (with 4 steps per k_trace iteration on coarse 3D grids: 20 there, with theta batches of 8 --
+    // the cloudy calls +1.8 %, two runs; profiles/r04/ab/cloudy_refill_gbatch_theta2.txt)
+    const bool coarse3d = grid3d && T.ncell < 4096;
+    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? (coarse3d ? 20 : 16) : 28);
     // ended chains' list appends at the wave's next refill (kernel_trace.hpp `append`): ray3d
     // +3.7 %, hg +5.1 %, iso +2.7 %, the cloudy configs[3] calls +3.4-3.8 % (3e8 / 1e8 packets,
     // profiles/r03/late_append_ab.txt)
@@ -788,7 +791,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // this many lanes of the wave need that evaluation (or few lanes still step), so the
     // wave runs the theta / phi form in fewer iterations
     const char* gb = getenv("ARTES_GBATCH");
-    R.gbatch = gb ? std::max(1, std::min(64, atoi(gb))) : 4;
+    R.gbatch = gb ? std::max(1, std::min(64, atoi(gb))) : (coarse3d ? 8 : 4);
     // the least list entries a dynamic grab of k_trace asks for (the wave keeps the rest for
     // its next refills; kernel_event.hpp, wave_take): 128 (profiles/r04/ab/dyn_grab_sweep*.txt)
     const char* dg = getenv("ARTES_DGRAB");
