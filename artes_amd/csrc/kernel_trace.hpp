@@ -993,6 +993,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         // compare per copy, cost ray3d 3 %.)
 #pragma unroll
         for (int rep = 0; rep < NREP; rep++) {
+        TM_TICK(t_rep);   // (timing build: the evaluation is timed from each step's start)
         if (have && !parked && !end) {
             const double k = kext;
             // ------------------------------------------- evaluate one face family
@@ -1107,7 +1108,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #endif
             }   // run_eval
             TM_TICK(tev);
-            TM_ADD(2, tev - t2);
+            TM_ADD(2, tev - t_rep);
             // ---------------------------------------------------- trace step
             // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
             // The nearest distance of the three is the reference's choice whenever it
