@@ -63,6 +63,15 @@ def test_k_trace_budgets():
         assert r["vgpr_count"] <= 102, (name, r)
 
 
+def test_k_trace_step_counts():
+    # steps per loop iteration: 8 on fine 3D and radial-only grids, 4 on coarse
+    # 3D grids -- both 3D instantiations and the radial-only one with 8 must be in the library
+    ks = _kernels()
+    _find(ks, "_ZN5artes7k_traceILb1ELb0ELi4ELb0ELi8E")
+    _find(ks, "_ZN5artes7k_traceILb1ELb0ELi4ELb0ELi4E")
+    _find(ks, "_ZN5artes7k_traceILb0ELb0ELi4ELb0ELi8E")
+
+
 def test_k_event_and_k_emit_budgets():
     ks = _kernels()
     for name, r in _find(ks, "_ZN5artes7k_event").items():
