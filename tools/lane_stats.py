@@ -3,8 +3,8 @@ usage: python tools/lane_stats.py [packets] [ENV=VAL,ENV=VAL ...]  (one variant 
 LS_WORKLOAD=cloudy: the configs[3] cloudy atmosphere (synthetic.make_cloudy, 0.45 micron, the
 `phase` mode's 1-pixel detector at 0 degrees) instead of ray3d.
 Since round 4 an iteration runs several steps ("Several steps per iteration"):
-the per-iteration stop / move / retry counters then describe the iteration's last step only;
-run with ARTES_STEPS=... on a build of one step per iteration for the round-3 meaning."""
+the per-iteration stop / move / retry counters then describe the iteration's last step only
+(wave-steps, lanes and refills stay per iteration)."""
 import os
 import sys
 
