@@ -13,7 +13,7 @@ import numpy as np
 ARTES_NUM_ERR = 64
 ARTES_NUM_COUNTERS = 8
 ARTES_NUM_TOTALS = 10      # [0..3] sum T_p, [4..7] sum T_p^2, [8] flux_emitted, [9] flux_exit
-ARTES_ABI_VERSION = 5
+ARTES_ABI_VERSION = 6
 ARTES_TRACE_FIELDS = 8    # artes_run_trace record: I, scatters, crossings, end state, -Q, U, V, 0
 COUNTER_NAMES = ("crossings", "scatters", "peels", "packets", "exited", "absorbed", "dropped", "detected")
 

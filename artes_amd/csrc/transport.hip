@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -83,8 +84,55 @@ __global__ void reduce_detector(const double* __restrict__ copies, size_t stride
 // ================================================================= C ABI ===
 using namespace artes;
 
+// ----------------------------------------------------------- schedule tuning ---
+// Launch-schedule overrides of one grid handle (artes_set_tuning).  Every default below is
+// the measured optimum, and no key except `engine` changes a per-packet result: they move
+// the schedule only (tests/test_gpu_engine.py).  The production library takes them through
+// that call alone -- it reads no environment variable, so a stray variable in a user's shell
+// cannot change the schedule or the engine.  The development build (-DARTES_DEV_KNOBS,
+// libartes_hip_dev.so, and the ARTES_DEBUG test build) also takes ARTES_<KEY> from the
+// environment at grid creation, for the A/B tools under tools/.
+enum TuneKey : int {
+    T_ENGINE, T_POOL, T_STEPS, T_REFILL, T_STATIC, T_DGRAB, T_BATCH, T_BATCH_MIN, T_HBATCH, T_GBATCH, T_DEFER,
+    T_BACKWARD, T_EMIT_FIRST, T_LATE_APPEND, T_PIX1, T_DET_LDS, T_EVENT_LDS, T_EVENT_LDSC, T_EVENT_BLOCK, T_EVENT_BPC,
+    T_TRACE_BPC, T_WPE, T_MSYM, T_MAX_IT, T_VERBOSE, T_NUM
+};
+struct TuneSpec {
+    const char* name;
+    long long lo, hi;   // accepted range ("steps": 4 or 8; "event_block": 256 or 768)
+};
+static const TuneSpec TUNE[T_NUM] = {
+    {"engine", 0, 1},            // 0 the event engine, 1 the fused persistent engine (comparison tests)
+    {"pool", 1024, 1LL << 26},   // packet-pool slots (default 131072 per CU)
+    {"steps", 4, 8},             // k_trace steps per loop iteration on 3D grids: 4 or 8
+    {"refill", 1, 64},           // k_trace: refill a wave once this many lanes are idle
+    {"static", 0, 64},           // statically dealt share of the trace list, in 1/64
+    {"dgrab", 1, 4096},          // least list entries of a dynamic grab
+    {"batch", 1, 64},            // batched forced first interaction: lanes that wait
+    {"batch_min", 1, 64},        // ... or fewer than this many lanes still step
+    {"hbatch", 1, 64},           // batched interaction + peel set-up: lanes that wait
+    {"gbatch", 1, 64},           // batched theta evaluations: lanes that wait
+    {"defer", 1, 64},            // persistent engine: event deferral
+    {"backward", 0, 1},          // backward walk after the forced first interaction
+    {"emit_first", 0, 1},        // trace-list order
+    {"late_append", 0, 1},       // list appends of ended chains at the wave's next refill
+    {"pix1", 0, 1},              // one-pixel detectors: per-lane sums
+    {"det_lds", 0, 1},           // k_event detector in LDS
+    {"event_lds", 0, 1},         // k_event scattering tables in LDS
+    {"event_ldsc", 0, 1},        // k_event cumulative tables alone in LDS
+    {"event_block", 256, 768},   // k_event block: 256 or 768 threads
+    {"event_bpc", 1, 16},        // k_event blocks per CU (LDS-detector kernels)
+    {"trace_bpc", 1, 16},        // k_trace blocks per CU
+    {"wpe", 3, 4},               // k_trace occupancy target (waves per SIMD)
+    {"msym", 0, 1},              // block-diagonal matrices read as 4 elements per row
+    {"max_it", 1, 1LL << 40},    // engine iterations before a call fails
+    {"verbose", 0, 1},           // one stderr line per call (pool, iterations, kernel choice)
+};
+
 struct artes_grid {
     int device = 0;
+    long long tune[T_NUM];   // -1: the default (artes_set_tuning)
+    artes_grid() { std::fill(tune, tune + T_NUM, -1LL); }
     HostTables T;
     double *d_rf2 = nullptr, *d_thetaf = nullptr, *d_tan2 = nullptr, *d_phif = nullptr, *d_phis = nullptr,
            *d_phic = nullptr, *d_kappa = nullptr, *d_albedo = nullptr, *d_ka = nullptr, *d_mats = nullptr, *d_cums = nullptr,
@@ -123,6 +171,9 @@ struct artes_grid {
     int* h_count = nullptr;               // pinned
     hipEvent_t ev_poll = nullptr;
     int trace_blocks = 0;
+    int trace_nrep = 0;                   // steps per iteration of the last k_trace launched
+    std::string last_trace, last_event;   // the kernel instantiations of the last call (artes_last_launch)
+    std::string launch_info;
     long long last_iterations = 0;
     // occupancy answers per (kernel, dynamic LDS bytes), queried once per grid
     std::vector<std::pair<std::pair<const void*, size_t>, int>> occ;
@@ -142,6 +193,25 @@ struct artes_grid {
     std::vector<int> prof_kind;
     size_t prof_used = 0;
 };
+
+// a tuning value of the handle, or `def` when it was not set
+static long long tv(const artes_grid* g, int k, long long def) { return g->tune[k] >= 0 ? g->tune[k] : def; }
+
+#ifdef ARTES_DEV_KNOBS
+// development build: ARTES_<KEY> from the environment at grid creation (ARTES_ENGINE=persistent)
+static void tuning_from_env(artes_grid* g) {
+    for (int k = 0; k < T_NUM; k++) {
+        std::string var = "ARTES_";
+        for (const char* c = TUNE[k].name; *c; c++) var += (char)toupper(*c);
+        const char* e = getenv(var.c_str());
+        if (!e) continue;
+        const long long v = k == T_ENGINE ? (std::string(e) == "persistent" ? 1 : 0) : atoll(e);
+        g->tune[k] = std::max(TUNE[k].lo, std::min(TUNE[k].hi, v));
+        if (k == T_STEPS) g->tune[k] = v == 4 ? 4 : 8;
+        if (k == T_EVENT_BLOCK) g->tune[k] = v == 256 ? 256 : 768;
+    }
+}
+#endif
 
 // resident blocks per CU of `kernel` at `lds` bytes of dynamic LDS (cached per grid: the
 // event engine launches the same few kernels hundreds of times per call)
@@ -201,7 +271,35 @@ extern "C" {
 int32_t artes_abi_version(void) { return ARTES_ABI_VERSION; }
 
 const char* artes_build_info(void) {
+#ifdef ARTES_DEV_KNOBS
+    return "artes_amd transport engine: gfx950 HIP, FP64, event engine (k_trace / k_event / k_emit), NCOPY=8; "
+           "development build: tuning also from ARTES_* environment variables";
+#else
     return "artes_amd transport engine: gfx950 HIP, FP64, event engine (k_trace / k_event / k_emit), NCOPY=8";
+#endif
+}
+
+int32_t artes_set_tuning(artes_grid* g, const char* key, int64_t value) {
+    if (!g || !key) return fail(-22, "null argument");
+    for (int k = 0; k < T_NUM; k++) {
+        if (std::strcmp(key, TUNE[k].name) != 0) continue;
+        if (value < 0) { g->tune[k] = -1; return 0; }   // back to the default
+        if (value < TUNE[k].lo || value > TUNE[k].hi || (k == T_STEPS && value != 4 && value != 8) ||
+            (k == T_EVENT_BLOCK && value != 256 && value != 768))
+            return fail(-22, std::string("tuning value out of range for ") + key);
+        if (k == T_STEPS && !(g->T.ntheta > 1 || g->T.nphi > 1) && value != 8)
+            return fail(-22, "steps: radial-only grids have the 8-step k_trace only");
+        g->tune[k] = value;
+        return 0;
+    }
+    return fail(-22, std::string("unknown tuning key ") + key);
+}
+
+int64_t artes_get_tuning(const artes_grid* g, const char* key) {
+    if (!g || !key) return -22;
+    for (int k = 0; k < T_NUM; k++)
+        if (std::strcmp(key, TUNE[k].name) == 0) return g->tune[k];
+    return -22;
 }
 
 const char* artes_last_error(void) { return g_last_error.c_str(); }
@@ -281,6 +379,9 @@ int32_t artes_grid_create(const artes_grid_desc* desc, int32_t device, artes_gri
     g->max_blocks = std::max(1, per_cu) * prop.multiProcessorCount;
     g->num_cus = prop.multiProcessorCount;
     HIP_TRY(hipDeviceSynchronize());
+#ifdef ARTES_DEV_KNOBS
+    tuning_from_env(g.get());
+#endif
     *out = g.release();
     return 0;
 }
@@ -354,10 +455,7 @@ static int32_t wl_set(artes_grid* g, int wl, artes_grid::WlSet** out) {
     return 0;
 }
 
-static bool use_event_engine() {
-    const char* e = getenv("ARTES_ENGINE");
-    return !(e && std::string(e) == "persistent");
-}
+static bool use_event_engine(const artes_grid* g) { return tv(g, T_ENGINE, 0) == 0; }
 
 // allocate the packet pool (transport and diagnostic records) and the work lists of the
 // event engine, sized for a call of n packets: a call queues at most n slots, so the pool
@@ -373,14 +471,13 @@ static void free_pool(artes_grid* g) {
 }
 
 static int32_t ensure_pool(artes_grid* g, uint64_t n) {
-    const char* env = getenv("ARTES_POOL");
     // 128 Ki slots per CU (33.6 M on MI355X; 4.3 GB of transport records + 4.3 GB of
     // diagnostic ones): every k_trace launch ends in a tail of a few long traces
     // (~0.35 ms), so fewer, larger iterations pay it less often.  With one pool the random
     // record accesses of k_event and k_emit missed in the TLBs past ~30 M slots; split
     // over the XCDs (NSUB sub-engines) they no longer do up to 50 M (pool sweep in
     // DESIGN.md §3)
-    long long P = env ? atoll(env) : (long long)g->num_cus * 131072;
+    long long P = tv(g, T_POOL, (long long)g->num_cus * 131072);
     P = std::max<long long>(1024, std::min<long long>(P, 1LL << 26));
     P = std::min<long long>(P, std::max<long long>((long long)std::min<uint64_t>(n, 1ULL << 26), 1024));
     P = (P + 64 * NSUB - 1) / (64 * NSUB) * (64 * NSUB);   // NSUB sub-engines of whole waves of slots
@@ -421,6 +518,12 @@ static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun&
     const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
     const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW, NREP>, lds);
     g->trace_blocks = round_sub(per_cu * g->num_cus);
+    g->trace_nrep = NREP;
+    if (g->last_trace.empty()) {
+        char b[80];
+        snprintf(b, sizeof(b), "k_trace<%d,%d,%d,%d,%d>", (int)G3D, (int)OBL, WPE, (int)FLOW, NREP);
+        g->last_trace = b;
+    }
     timed(g, ARTES_K_TRACE, stream, [&] {
         hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW, NREP>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
@@ -492,44 +595,36 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     int* cnt = g->d_counts;
     const int side_blocks = round_sub(g->num_cus * 8);
     // launch knobs, read once per call (tuning overrides; the defaults are the measured optima)
-    const char* we = getenv("ARTES_WPE");
-    const int wpe = we ? atoi(we) : 4;
-    const char* bp = getenv("ARTES_TRACE_BPC");   // k_trace blocks per CU
-    const int trace_bpc = bp ? std::max(1, atoi(bp)) : 0;
+    const int wpe = (int)tv(g, T_WPE, 4);
+    const int trace_bpc = (int)tv(g, T_TRACE_BPC, 0);   // k_trace blocks per CU (0: the occupancy limit)
     // k_trace steps per loop iteration ("Several steps per iteration"): 8 on fine
     // 3D and radial-only grids, 4 on coarse 3D grids (< 4096 cells), whose short chains leave
     // more lanes idle for the rest of an iteration (profiles/r04/ab/trace_nrep*_ab.txt);
-    // ARTES_STEPS=4|8 overrides (3D grids)
-    const char* ts = getenv("ARTES_STEPS");
-    const int trace_steps = ts ? (atoi(ts) == 4 ? 4 : 8) : (G.ncell < 4096 ? 4 : 8);
+    // tuning "steps" = 4 | 8 overrides (3D grids; the oblate, flow and wpe = 3 kernels have 8)
+    const int trace_steps = (int)tv(g, T_STEPS, G.ncell < 4096 ? 4 : 8);
     if (trace_table_bytes(G.nr, G.ntheta, G.nphi) > 65536) return fail(-22, "face tables exceed the 64 KiB LDS budget of k_trace");
     // scattering tables in LDS for k_event when they fit next to one another (a few
     // distinct matrices: uniform and layered atmospheres); otherwise read from L2
     const size_t ev_bytes = event_table_doubles(G.nmat, G.msym != 0) * sizeof(double);
-    const char* el = getenv("ARTES_EVENT_LDS");
-    const bool ev_lds = (el ? atoi(el) != 0 : true) && ev_bytes <= 65536;
+    const bool ev_lds = tv(g, T_EVENT_LDS, 1) != 0 && ev_bytes <= 65536;
     // planes 0-8 of the detector accumulated per k_event block in LDS when they fit
     // (the I-only count plane 9 of the rare thermal / surface peels goes straight to HBM):
     // with the scattering tables, 76.7 KB at 25x25 pixels, so two blocks share a CU
     const size_t det_bytes = 9 * (size_t)R.nx * R.ny * sizeof(double);
     // one-pixel detector (spectrum / phase): per-lane register sums reduced over the wave
-    // (k_event PIX1) instead of same-address atomics; ARTES_PIX1=0 turns it off
-    const char* p1 = getenv("ARTES_PIX1");
-    const bool pix1 = (p1 ? atoi(p1) != 0 : true) && R.nx == 1 && R.ny == 1;
+    // (k_event PIX1) instead of same-address atomics; tuning "pix1" = 0 turns it off
+    const bool pix1 = tv(g, T_PIX1, 1) != 0 && R.nx == 1 && R.ny == 1;
     // k_event's block with both the tables and the detector in LDS: EVB threads, one block
     // (12 waves, 3 per SIMD at <= 170 VGPRs) per CU sharing one LDS copy, instead of two
     // 256-thread blocks (2 waves per SIMD, LDS-bound): k_event -7 % on ray3d / hg / iso
-    // (ARTES_EVENT_BLOCK=256 for the old shape)
-    const char* ebs = getenv("ARTES_EVENT_BLOCK");
-    const int ev_block = ebs && atoi(ebs) == 256 ? 256 : EVB;
+    // (tuning "event_block" = 256 for the old shape)
+    const int ev_block = tv(g, T_EVENT_BLOCK, EVB) == 256 ? 256 : EVB;
     // matrices too many for LDS: their cumulative tables alone in LDS (k_event LDS_C) when
     // they fit beside the detector or the one-pixel lane slots in one EVB-thread block per
-    // CU; ARTES_EVENT_LDSC=0 turns it off
-    const char* elc = getenv("ARTES_EVENT_LDSC");
+    // CU; tuning "event_ldsc" = 0 turns it off
     const size_t cum_bytes = event_cum_doubles(G.nmat) * sizeof(double);
-    const bool ev_ldsc_ok = !ev_lds && ev_block == EVB && (elc ? atoi(elc) != 0 : true);
-    const char* dl = getenv("ARTES_DET_LDS");
-    const bool det_lds = !pix1 && (dl ? atoi(dl) != 0 : true) && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
+    const bool ev_ldsc_ok = !ev_lds && ev_block == EVB && tv(g, T_EVENT_LDSC, 1) != 0;
+    const bool det_lds = !pix1 && tv(g, T_DET_LDS, 1) != 0 && (ev_lds ? ev_bytes : 0) + det_bytes <= 98304;
     const size_t lds_cap = 160 * 1024 - 4096;   // (a margin for static LDS)
     const bool ev_ldsc = ev_ldsc_ok && cum_bytes + (pix1 ? pix1_slot_bytes(EVB) : det_lds ? det_bytes : 0) <= lds_cap;
     const size_t tab_bytes = ev_lds ? ev_bytes : (ev_ldsc ? cum_bytes : 0);
@@ -540,8 +635,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
                                                : ev_ldsc ? blocks_per_cu(g, k_event<false, true, false, EVB, true>, b, EVB)
                                                          : blocks_per_cu(g, k_event<false, true, false, EVB>, b, EVB))
                                      : (ev_lds ? blocks_per_cu(g, k_event<true, true>, b) : blocks_per_cu(g, k_event<false, true>, b));
-        const char* eb = getenv("ARTES_EVENT_BPC");
-        if (eb) per_cu = std::max(1, atoi(eb));
+        per_cu = (int)tv(g, T_EVENT_BPC, per_cu);
         ev_blocks = round_sub(per_cu * g->num_cus);
     }
     // the one-pixel kernel in EVB-thread blocks too: the launch bound holds it to 3 waves per
@@ -599,29 +693,57 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
             hipLaunchKernelGGL(k_rotate, dim3(NSUB), dim3(64), 0, stream, cnt, 1, g->d_grab, g->d_next, R.emit_first, 2 * Ps, R.err);
         });
     }
+    // The k_event instantiation of this call (fixed for the call; its name is reported by
+    // artes_last_launch): tables in LDS (LDS_T) or only their cumulative part (LDS_C), the
+    // detector in LDS (LDS_D) or per-lane one-pixel sums (PIX1), 768- or 256-thread blocks.
+    // tests/test_gpu_event_variants.py forces every branch and checks it against the oracle.
+    int ev_v = 13;
+    if (pix1_big && ev_lds) ev_v = 1;
+    else if (pix1_big && ev_ldsc) ev_v = 2;
+    else if (det_lds && ev_ldsc) ev_v = 3;
+    else if (glob_ldsc) ev_v = 4;
+    else if (pix1_big) ev_v = 5;
+    else if (pix1 && ev_lds) ev_v = 6;
+    else if (pix1) ev_v = 7;
+    else if (ev_lds && det_lds && ev_block == EVB) ev_v = 8;
+    else if (ev_lds && det_lds) ev_v = 9;
+    else if (ev_lds) ev_v = 10;
+    else if (det_lds && ev_block == EVB) ev_v = 11;
+    else if (det_lds) ev_v = 12;
+    static const struct { int lt, ld, p1, big, lc; } EVV[14] = {
+        {0, 0, 0, 0, 0}, {1, 0, 1, 1, 0}, {0, 0, 1, 1, 1}, {0, 1, 0, 1, 1}, {0, 0, 0, 1, 1}, {0, 0, 1, 1, 0}, {1, 0, 1, 0, 0},
+        {0, 0, 1, 0, 0}, {1, 1, 0, 1, 0}, {1, 1, 0, 0, 0}, {1, 0, 0, 0, 0}, {0, 1, 0, 1, 0}, {0, 1, 0, 0, 0}, {0, 0, 0, 0, 0}};
+    {
+        char b[96];
+        snprintf(b, sizeof(b), "k_event<%d,%d,%d,%d,%d>", EVV[ev_v].lt, EVV[ev_v].ld, EVV[ev_v].p1, EVV[ev_v].big ? EVB : BLOCK,
+                 EVV[ev_v].lc);
+        g->last_event = b;
+    }
+    auto launch_event = [&](const SubLists& L) {
+        switch (ev_v) {
+        case 1: hipLaunchKernelGGL((k_event<true, false, true, EVB>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L); break;
+        case 2: hipLaunchKernelGGL((k_event<false, false, true, EVB, true>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L); break;
+        case 3: hipLaunchKernelGGL((k_event<false, true, false, EVB, true>), dim3(ev_blocks), dim3(EVB), cum_bytes + det_bytes, stream, G, R, g->pool, L); break;
+        case 4: hipLaunchKernelGGL((k_event<false, false, false, EVB, true>), dim3(ev_blocks), dim3(EVB), cum_bytes, stream, G, R, g->pool, L); break;
+        case 5: hipLaunchKernelGGL((k_event<false, false, true, EVB>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L); break;
+        case 6: hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L); break;
+        case 7: hipLaunchKernelGGL((k_event<false, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L); break;
+        case 8: hipLaunchKernelGGL((k_event<true, true, false, EVB>), dim3(ev_blocks), dim3(EVB), ev_bytes + det_bytes, stream, G, R, g->pool, L); break;
+        case 9: hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L); break;
+        case 10: hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L); break;
+        case 11: hipLaunchKernelGGL((k_event<false, true, false, EVB>), dim3(ev_blocks), dim3(EVB), det_bytes, stream, G, R, g->pool, L); break;
+        case 12: hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L); break;
+        default: hipLaunchKernelGGL((k_event<false, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L); break;
+        }
+    };
     HIP_TRY(hipGetLastError());
     int in = 0;
     long long it = 0;
-    const char* mi = getenv("ARTES_MAX_IT");
-    const long long max_it = mi ? atoll(mi) : 2000000LL;
+    const long long max_it = tv(g, T_MAX_IT, 2000000LL);
     for (;;) {
         SubLists L = lists(in);
         launch_trace_any<G3D>(g, wpe, trace_steps, trace_bpc, G, R, L, stream);
-        timed(g, ARTES_K_EVENT, stream, [&] {
-            if (pix1_big && ev_lds) hipLaunchKernelGGL((k_event<true, false, true, EVB>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L);
-            else if (pix1_big && ev_ldsc) hipLaunchKernelGGL((k_event<false, false, true, EVB, true>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L);
-            else if (det_lds && ev_ldsc) hipLaunchKernelGGL((k_event<false, true, false, EVB, true>), dim3(ev_blocks), dim3(EVB), cum_bytes + det_bytes, stream, G, R, g->pool, L);
-            else if (glob_ldsc) hipLaunchKernelGGL((k_event<false, false, false, EVB, true>), dim3(ev_blocks), dim3(EVB), cum_bytes, stream, G, R, g->pool, L);
-            else if (pix1_big) hipLaunchKernelGGL((k_event<false, false, true, EVB>), dim3(ev_blocks), dim3(EVB), p1_bytes, stream, G, R, g->pool, L);
-            else if (pix1 && ev_lds) hipLaunchKernelGGL((k_event<true, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L);
-            else if (pix1) hipLaunchKernelGGL((k_event<false, false, true>), dim3(side_blocks), dim3(BLOCK), p1_bytes, stream, G, R, g->pool, L);
-            else if (ev_lds && det_lds && ev_block == EVB) hipLaunchKernelGGL((k_event<true, true, false, EVB>), dim3(ev_blocks), dim3(EVB), ev_bytes + det_bytes, stream, G, R, g->pool, L);
-            else if (ev_lds && det_lds) hipLaunchKernelGGL((k_event<true, true>), dim3(ev_blocks), dim3(BLOCK), ev_bytes + det_bytes, stream, G, R, g->pool, L);
-            else if (ev_lds) hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L);
-            else if (det_lds && ev_block == EVB) hipLaunchKernelGGL((k_event<false, true, false, EVB>), dim3(ev_blocks), dim3(EVB), det_bytes, stream, G, R, g->pool, L);
-            else if (det_lds) hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L);
-            else hipLaunchKernelGGL((k_event<false, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L);
-        });
+        timed(g, ARTES_K_EVENT, stream, [&] { launch_event(L); });
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
             hipLaunchKernelGGL(k_rotate, dim3(NSUB), dim3(64), 0, stream, cnt, in, g->d_grab, g->d_next, R.emit_first, 2 * Ps, R.err);
@@ -643,14 +765,14 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
             if (live == 0) break;
         }
         if (it > max_it) {
-            if (getenv("ARTES_VERBOSE")) dump_live(g, cnt, in, stream);
+            if (tv(g, T_VERBOSE, 0)) dump_live(g, cnt, in, stream);
             return fail(-5, "event engine did not terminate");
         }
     }
     g->last_iterations = it;
-    if (getenv("ARTES_VERBOSE"))
-        fprintf(stderr, "[artes] event engine: pool %d, %lld iterations, trace blocks %d, event blocks %d (LDS tables %d, cumulative tables %d, detector %d, 1-pixel %d, matrices %d)\n",
-                P, it, g->trace_blocks, ev_blocks, (int)ev_lds, (int)ev_ldsc, (int)det_lds, (int)pix1, G.nmat);
+    if (tv(g, T_VERBOSE, 0))
+        fprintf(stderr, "[artes] event engine: pool %d, %lld iterations, trace blocks %d (%d steps per iteration), event blocks %d (LDS tables %d, cumulative tables %d, detector %d, 1-pixel %d, matrices %d)\n",
+                P, it, g->trace_blocks, g->trace_nrep, ev_blocks, (int)ev_lds, (int)ev_ldsc, (int)det_lds, (int)pix1, G.nmat);
     return 0;
 }
 
@@ -661,8 +783,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
                       double* rec, hipStream_t stream, double* flow_g = nullptr, double* flow_t = nullptr) {
     const HostTables& T = g->T;
     if (!p) return fail(-22, "null params");
+    g->last_trace.clear();
+    g->last_event.clear();
     if (p->photon_source != 1 && p->photon_source != 2) return fail(-22, "photon_source must be 1 (star) or 2 (planet)");
-    if (!use_event_engine() && (p->photon_source != 1 || p->surface_albedo > 0.0 || flow_g || flow_t))
+    if (!use_event_engine(g) && (p->photon_source != 1 || p->surface_albedo > 0.0 || flow_g || flow_t))
         return fail(-38, "the persistent engine supports the star source without surface reflection or flow output only");
     if (p->wl_index < 0 || p->wl_index >= T.nwav) return fail(-22, "wl_index out of range");
     if (p->nx < 1 || p->ny < 1 || (size_t)p->nx * p->ny > (1u << 26)) return fail(-22, "bad detector size");
@@ -738,9 +862,8 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
         const int32_t rc = wl_set(g, p->wl_index, &W);
         if (rc) return rc;
         G.nmat = W->nmat; G.matid = W->d_matid; G.cums = W->d_cums;
-        // (the persistent engine reads the 16-element form; ARTES_MSYM=0, read per call, too)
-        const char* ms = getenv("ARTES_MSYM");
-        G.msym = (W->d_mats4 && use_event_engine() && !(ms && atoi(ms) == 0)) ? 1 : 0;
+        // (the persistent engine reads the 16-element form; tuning "msym" = 0, read per call, too)
+        G.msym = (W->d_mats4 && use_event_engine(g) && tv(g, T_MSYM, 1) != 0) ? 1 : 0;
         G.mats = G.msym ? W->d_mats4 : W->d_mats;
     }
     G.sc2 = g->d_sc2; G.ss2 = g->d_ss2;
@@ -751,9 +874,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.photon_source = p->photon_source; R.photon_emission = p->photon_emission; R.photon_bias = p->photon_bias;
     R.moments = p->packet_moments != 0 || rec != nullptr;
     R.stellar_direction = p->stellar_direction;
-    const char* env = getenv("ARTES_DEFER");
-    R.defer = env ? atoi(env) : 16;
-    const char* rf = getenv("ARTES_REFILL");
+    R.defer = (int)tv(g, T_DEFER, 16);
     // refill a wave once this many of its lanes are idle (re-swept after the batched
     // interactions: 16 on 3D grids, 20 on radial-only ones)
     const bool grid3d = (T.ntheta > 1 || T.nphi > 1);
@@ -765,42 +886,34 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // (with 4 steps per k_trace iteration on coarse 3D grids: 20 there, with theta batches of 8 --
     // the cloudy calls +1.8 %, two runs; profiles/r04/ab/cloudy_refill_gbatch_theta2.txt)
     const bool coarse3d = grid3d && T.ncell < 4096;
-    R.refill = rf ? std::max(1, std::min(64, atoi(rf))) : (grid3d ? (coarse3d ? 20 : 16) : 28);
+    R.refill = (int)tv(g, T_REFILL, grid3d ? (coarse3d ? 20 : 16) : 28);
     // ended chains' list appends at the wave's next refill (kernel_trace.hpp `append`): ray3d
     // +3.7 %, hg +5.1 %, iso +2.7 %, the cloudy configs[3] calls +3.4-3.8 % (3e8 / 1e8 packets,
     // profiles/r03/late_append_ab.txt)
-    const char* la = getenv("ARTES_LATE_APPEND");
-    R.late_append = la ? (atoi(la) != 0) : 1;
-    const char* ef = getenv("ARTES_EMIT_FIRST");
-    R.emit_first = ef ? (atoi(ef) != 0) : !grid3d;
-    const char* bw = getenv("ARTES_BACKWARD");
-    R.backward = bw ? (atoi(bw) != 0) : 1;
+    R.late_append = (int)tv(g, T_LATE_APPEND, 1);
+    R.emit_first = (int)tv(g, T_EMIT_FIRST, grid3d ? 0 : 1);
+    R.backward = (int)tv(g, T_BACKWARD, 1);
     // lanes that park for the batched forced first interaction (kernel_trace.hpp): run the
     // block once this many wait, or once fewer than batch_min lanes still step
-    const char* bt = getenv("ARTES_BATCH");
-    R.batch = bt ? std::max(1, std::min(64, atoi(bt))) : 1;
-    const char* bm = getenv("ARTES_BATCH_MIN");
-    R.batch_min = bm ? std::max(0, std::min(64, atoi(bm))) : 16;
+    R.batch = (int)tv(g, T_BATCH, 1);
+    // (>= 1: a wave whose stepping lanes all wait for a batch must run it)
+    R.batch_min = (int)tv(g, T_BATCH_MIN, 16);
     // lanes whose propagation reached its interaction point park the same way: the
     // interaction block (roulette, albedo weight, peel-off set-up) runs once this many wait
     // (6 on 3D grids, where the block also computes the peel-off trace's set-up bounds; 4 on
     // radial-only ones; profiles/r02/refill_hbatch_sweep*.txt)
-    const char* hb = getenv("ARTES_HBATCH");
-    R.hbatch = hb ? std::max(1, std::min(64, atoi(hb))) : (grid3d ? 6 : 4);
+    R.hbatch = (int)tv(g, T_HBATCH, grid3d ? 6 : 4);
     // trace-relative kernels: a lane whose nearest entry is a theta / phi bound waits until
     // this many lanes of the wave need that evaluation (or few lanes still step), so the
     // wave runs the theta / phi form in fewer iterations
-    const char* gb = getenv("ARTES_GBATCH");
-    R.gbatch = gb ? std::max(1, std::min(64, atoi(gb))) : (coarse3d ? 8 : 4);
+    R.gbatch = (int)tv(g, T_GBATCH, coarse3d ? 8 : 4);
     // the least list entries a dynamic grab of k_trace asks for (the wave keeps the rest for
     // its next refills; kernel_event.hpp, wave_take): 128 (profiles/r04/ab/dyn_grab_sweep*.txt)
-    const char* dg = getenv("ARTES_DGRAB");
-    R.dgrab = dg ? std::max(1, std::min(4096, atoi(dg))) : 128;
+    R.dgrab = (int)tv(g, T_DGRAB, 128);
     // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
     // 32 on 3D grids, 24 on radial-only ones since the dynamic grabs ask for 128 entries
     // (48 / 40 before: each grab was an atomic round trip; profiles/r04/ab/dyn_grab_sweep2_static.txt)
-    const char* sq = getenv("ARTES_STATIC");
-    R.static_q64 = sq ? std::max(0, std::min(64, atoi(sq))) : (grid3d ? 32 : 24);
+    R.static_q64 = (int)tv(g, T_STATIC, grid3d ? 32 : 24);
     R.det0 = sin(p->det_theta) * cos(p->det_phi);   // spherical_cartesian (ARTES.f90:495)
     R.det1 = sin(p->det_theta) * sin(p->det_phi);
     R.det2 = cos(p->det_theta);
@@ -819,7 +932,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
 
     const bool g3d = (T.ntheta > 1 || T.nphi > 1);
     HIP_TRY(hipEventRecord(g->ev0, stream));
-    if (n > 0 && use_event_engine()) {
+    if (n > 0 && use_event_engine(g)) {
         if (T.nr >= 4096 || T.ntheta >= 1024 || T.nphi >= 1024)
             return fail(-22, "event engine packs cells into 12/10/10 bits: nr < 4096, ntheta < 1024, nphi < 1024");
         if ((long long)T.ncell >= (1LL << 28))
@@ -986,6 +1099,12 @@ int32_t artes_run_trace(artes_grid* g, const artes_run_params* p, uint64_t first
     return run_host(g, p, first, n, seed, det.data(), nullptr, nullptr, nullptr, records);
 }
 
+const char* artes_last_launch(artes_grid* g) {
+    if (!g) return "";
+    g->launch_info = g->last_trace.empty() ? std::string("persistent") : g->last_trace + " " + g->last_event;
+    return g->launch_info.c_str();
+}
+
 int32_t artes_set_profiling(artes_grid* g, int32_t on) {
     if (!g) return fail(-22, "null grid");
     g->prof = on != 0;
@@ -999,9 +1118,13 @@ int32_t artes_kernel_times(artes_grid* g, double* ms, uint64_t* launches) {
     if (g->prof_used == 0) return 0;
     HIP_TRY(hipSetDevice(g->device));
     HIP_TRY(hipEventSynchronize(g->prof_ev[2 * g->prof_used - 1]));
-    // (development: ARTES_LAUNCH_LOG=<file> appends every launch's kind and time, one line per call)
+    // (development build: ARTES_LAUNCH_LOG=<file> appends every launch's kind and time, one line per call)
+#ifdef ARTES_DEV_KNOBS
     const char* log = getenv("ARTES_LAUNCH_LOG");
     FILE* lf = log ? fopen(log, "a") : nullptr;
+#else
+    FILE* lf = nullptr;
+#endif
     for (size_t i = 0; i < g->prof_used; i++) {
         float t = 0.0f;
         HIP_TRY(hipEventElapsedTime(&t, g->prof_ev[2 * i], g->prof_ev[2 * i + 1]));

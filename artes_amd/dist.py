@@ -16,9 +16,14 @@ CPU tests of this module.
 from __future__ import annotations
 
 import os
+import sys
 from dataclasses import dataclass
 
 import numpy as np
+
+# collectives this process issued, by path (tests/test_gpu_dist_cli.py checks that the RCCL
+# branch of allreduce_numpy ran): "host" (gloo, in place) and "device" (nccl, via the GPU)
+COLLECTIVES = {"host": 0, "device": 0}
 
 
 @dataclass
@@ -77,9 +82,17 @@ def shard(n_packets: int, rank: int, world: int) -> tuple[int, int]:
     return lo, hi - lo
 
 
+def group_active() -> bool:
+    """A process group is open (``init`` with several ranks, or one rank under
+    ARTES_DIST_FORCE=1): the reductions then go through it even at world size 1, so a
+    one-rank run exercises the collective path.  (No torch import when none was made.)"""
+    d = sys.modules.get("torch.distributed")
+    return d is not None and d.is_available() and d.is_initialized()
+
+
 def allreduce_numpy(arrays: list[np.ndarray], world: int) -> list[np.ndarray]:
-    """Sum host arrays over ranks (gloo / CPU path)."""
-    if world <= 1:
+    """Sum host arrays over ranks: in place under gloo, through the rank's GPU under nccl."""
+    if world <= 1 and not group_active():
         return arrays
     import torch
     import torch.distributed as dist
@@ -92,6 +105,7 @@ def allreduce_numpy(arrays: list[np.ndarray], world: int) -> list[np.ndarray]:
     if on_gpu:
         t = t.to(torch.device("cuda", torch.cuda.current_device()))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    COLLECTIVES["device" if on_gpu else "host"] += 1
     flat = t.cpu().numpy() if on_gpu else t.numpy()
     out, at = [], 0
     for a in arrays:
@@ -105,7 +119,7 @@ def broadcast_int(value: int, r: Rank) -> int:
     """Rank 0's non-negative ``value`` (< 2^64) on every rank: the clock seed of a CLI run
     must be the same on every shard, or the global packet ids would not map to one RNG
     stream set (the result would then depend on the rank start times)."""
-    if r.world <= 1:
+    if r.world <= 1 and not group_active():
         return int(value)
     parts = np.array([value >> 32, value & 0xFFFFFFFF], dtype=np.float64) if r.rank == 0 else np.zeros(2)
     (out,) = allreduce_numpy([parts], r.world)   # exact: each half < 2^32
@@ -117,7 +131,7 @@ def run_sharded(transport, n_packets: int, seed: int, r: Rank):
     the results over all ranks (host tensors; the GPU bench uses device tensors + RCCL)."""
     first, count = shard(n_packets, r.rank, r.world)
     res = transport(first, count, seed)
-    if r.world > 1:
+    if r.world > 1 or group_active():
         flows = [k for k in ("flow_global", "flow_latitudinal") if getattr(res, k, None) is not None]
         red = allreduce_numpy([res.det, res.totals, res.counters.astype(np.float64), res.err.astype(np.float64)]
                               + [getattr(res, k) for k in flows], r.world)

@@ -22,6 +22,10 @@ _lib = None
 
 
 KERNEL_NAMES = ("trace", "event", "emit", "aux", "persistent")   # ARTES_K_* order
+# artes_set_tuning keys (include/artes_amd.h; transport.hip, TUNE)
+TUNING_KEYS = ("engine", "pool", "steps", "refill", "static", "dgrab", "batch", "batch_min", "hbatch", "gbatch", "defer",
+               "backward", "emit_first", "late_append", "pix1", "det_lds", "event_lds", "event_ldsc", "event_block",
+               "event_bpc", "trace_bpc", "wpe", "msym", "max_it", "verbose")
 
 
 class EngineUnavailable(RuntimeError):
@@ -86,6 +90,12 @@ def lib():
     L.artes_set_profiling.argtypes = [C.c_void_p, C.c_int32]
     L.artes_kernel_times.restype = C.c_int32
     L.artes_kernel_times.argtypes = [C.c_void_p, dp, up]
+    L.artes_set_tuning.restype = C.c_int32
+    L.artes_set_tuning.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+    L.artes_get_tuning.restype = C.c_int64
+    L.artes_get_tuning.argtypes = [C.c_void_p, C.c_char_p]
+    L.artes_last_launch.restype = C.c_char_p
+    L.artes_last_launch.argtypes = [C.c_void_p]
     if L.artes_abi_version() != ARTES_ABI_VERSION:
         raise EngineUnavailable("ABI version mismatch")
     _lib = L
@@ -159,6 +169,27 @@ class Grid:
 
     def num_matrices(self) -> int:
         return lib().artes_grid_num_matrices(self.h)
+
+    def set_tuning(self, **kv) -> None:
+        """Schedule overrides of this handle (``artes_set_tuning``; keys ``TUNING_KEYS``, a value
+        of ``None`` or -1 restores the default, ``engine="persistent"`` selects the fused engine)."""
+        for k, v in kv.items():
+            if k == "engine" and isinstance(v, str):
+                v = {"event": 0, "persistent": 1}[v]
+            _check(lib().artes_set_tuning(self.h, k.encode(), -1 if v is None else int(v)), f"artes_set_tuning({k})")
+
+    def last_launch(self) -> str:
+        """The kernel instantiations of the last call (``artes_last_launch``)."""
+        return lib().artes_last_launch(self.h).decode()
+
+    def tuning(self) -> dict:
+        """The keys this handle overrides ({} in production)."""
+        out = {}
+        for k in TUNING_KEYS:
+            v = lib().artes_get_tuning(self.h, k.encode())
+            if v >= 0:
+                out[k] = int(v)
+        return out
 
     def run(self, params: RunParams, first: int, n: int, seed: int, flow_global: bool = False,
             flow_latitudinal: bool = False) -> RunResult:

@@ -212,6 +212,11 @@ def main() -> int:
     step_ms = [a.elapsed_time(b) for a, b in ev]
     ktimes = grid.kernel_times()   # {class: (summed ms over the timed steps, launches)}
     grid.set_profiling(False)
+    # what ran: the library build, the kernel instantiations of the timed calls and the schedule
+    # overrides of the handle (none in production: the library reads no environment variable)
+    from artes_amd import engine as _engine
+    engine_info = {"build": _engine.lib().artes_build_info().decode(), "kernels": grid.last_launch(),
+                   "tuning": grid.tuning(), "lib_md5": _md5(_engine.LIB_PATH)}
     if coll:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -349,6 +354,7 @@ def main() -> int:
                                   "step_ms_hip_events": round(float(np.mean(step_ms)), 3)},
                      "events_per_packet": {"crossings": round(C, 3), "scatters": round(S, 4), "peels": round(P, 4)}},
         "cpu_baseline": cpu,
+        "engine": engine_info,
         "parity": parity,
         "configs2_32x16x32": cfg2,
         # reference error codes (error.log numbers) logged in the timed steps, with their rate

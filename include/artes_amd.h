@@ -67,7 +67,7 @@
 extern "C" {
 #endif
 
-#define ARTES_ABI_VERSION 5
+#define ARTES_ABI_VERSION 6
 #define ARTES_NUM_TOTALS 10
 #define ARTES_NUM_ERR 64
 #define ARTES_ERR_WATCHDOG 57
@@ -225,7 +225,7 @@ double artes_last_kernel_ms(artes_grid* grid);
 #define ARTES_K_EVENT       1   /* k_event: peel-off contribution + scattering       */
 #define ARTES_K_EMIT        2   /* k_emit: packet close-out + emission               */
 #define ARTES_K_AUX         3   /* list rotation, pool init, detector-copy reduction */
-#define ARTES_K_PERSISTENT  4   /* the fused single-kernel engine (ARTES_ENGINE=persistent) */
+#define ARTES_K_PERSISTENT  4   /* the fused single-kernel engine (tuning "engine" = 1)  */
 #define ARTES_NUM_KERNELS   5
 int32_t artes_set_profiling(artes_grid* grid, int32_t on);
 int32_t artes_kernel_times(artes_grid* grid, double* ms, uint64_t* launches);
@@ -239,6 +239,27 @@ int32_t artes_kernel_times(artes_grid* grid, double* ms, uint64_t* launches);
 int32_t artes_run_trace(artes_grid* grid, const artes_run_params* params,
                         uint64_t first_packet, uint64_t n_packets, uint64_t seed,
                         double* records);
+
+/* Schedule tuning of one grid handle (development A/B runs and tests).  `key` names one
+ * launch-schedule setting; `value` >= 0 overrides it, -1 restores the default (the measured
+ * optimum).  No key except "engine" changes a per-packet result: they move the schedule only.
+ * Keys: engine (0 event engine, 1 the fused persistent engine), pool (slots), steps (k_trace
+ * steps per iteration, 4 or 8, 3D grids), refill, static, dgrab, batch, batch_min, hbatch,
+ * gbatch, defer, backward, emit_first, late_append, pix1, det_lds, event_lds, event_ldsc,
+ * event_block (256 or 768), event_bpc, trace_bpc, wpe (3 or 4), msym, max_it, verbose
+ * (transport.hip, TUNE).  Returns -22 for an unknown key or a value outside the key's range.
+ * The production library reads no environment variable: the reference's drop-in never sees
+ * a schedule it did not ask for.  The development build (libartes_hip_dev.so) also takes
+ * ARTES_<KEY> from the environment when a grid is created.
+ * artes_get_tuning returns the override of `key` (-1: the default) or -22. */
+int32_t artes_set_tuning(artes_grid* grid, const char* key, int64_t value);
+int64_t artes_get_tuning(const artes_grid* grid, const char* key);
+
+/* The kernel instantiations the last call on this grid launched, e.g.
+ * "k_trace<1,0,4,0,8> k_event<1,1,0,768,0>" (template arguments of kernel_trace.hpp /
+ * kernel_event.hpp: G3D, OBL, WPE, FLOW, NREP and LDS_T, LDS_D, PIX1, block, LDS_C), or
+ * "persistent"; storage owned by the grid, valid until its next call. */
+const char* artes_last_launch(artes_grid* grid);
 
 /* Last error message of the calling thread (static storage). */
 const char* artes_last_error(void);

@@ -61,12 +61,10 @@ def test_cloudy_trajectories_match_oracle(require_gpu, oracle_mod, cloudy, wl):
     assert (np.abs(ref[:, 6]) > 1e-6 * np.abs(ref[:, 0])).mean() > 0.1
 
 
-@pytest.mark.parametrize("knob", [("ARTES_DET_LDS", "0"), ("ARTES_EVENT_BLOCK", "256")])
+@pytest.mark.parametrize("knob", [("det_lds", 0), ("event_block", 256)])
 def test_cloudy_detector_lds_knob(require_gpu, cloudy, knob):
     """Detector accumulation in LDS or straight to HBM, and the LDS-detector k_event with L2
     tables (401 matrices) in 768- or 256-thread blocks: same packets, same image."""
-    import os
-
     from artes_amd.engine import Grid
 
     _, _, atm = cloudy
@@ -75,29 +73,21 @@ def test_cloudy_detector_lds_knob(require_gpu, cloudy, knob):
     grid = Grid(atm, device=0)
     p = driver.run_params(cfg, det, 1, cell_depth=grid.cell_depth(1))
     a = grid.run(p, 0, 200000, 5)
-    old = os.environ.get(knob[0])
-    os.environ[knob[0]] = knob[1]
-    try:
-        b = grid.run(p, 0, 200000, 5)
-    finally:
-        if old is None:
-            os.environ.pop(knob[0])
-        else:
-            os.environ[knob[0]] = old
+    la = grid.last_launch()
+    grid.set_tuning(**{knob[0]: knob[1]})
+    b = grid.run(p, 0, 200000, 5)
+    assert grid.last_launch() != la
     grid.close()
     np.testing.assert_allclose(b.det, a.det, rtol=1e-9, atol=1e-300)
     assert np.array_equal(b.counters, a.counters)
 
 
-@pytest.mark.parametrize("source,knob", [("star", ("ARTES_PIX1", "0")), ("planet", ("ARTES_PIX1", "0")),
-                                         ("star", ("ARTES_EVENT_BLOCK", "256"))])
+@pytest.mark.parametrize("source,knob", [("star", ("pix1", 0)), ("planet", ("pix1", 0)), ("star", ("event_block", 256))])
 def test_one_pixel_lane_sums_knob(require_gpu, cloudy, source, knob):
     """A one-pixel detector (spectrum / phase) keeps per-lane peel sums (LDS slots) reduced
     over the wave (k_event PIX1) instead of same-address atomics, in 768- or 256-thread
     blocks: same packets, same sums (to the summation order), counts exact; the planet
     source covers the I-only thermal peels."""
-    import os
-
     from artes_amd.engine import Grid
 
     _, _, atm = cloudy
@@ -111,11 +101,10 @@ def test_one_pixel_lane_sums_knob(require_gpu, cloudy, source, knob):
     grid = Grid(atm, device=0)
     p = driver.run_params(cfg, det, 0, det_phi=math.radians(40.0), cell_depth=-1 if source == "planet" else grid.cell_depth(0))
     a = grid.run(p, 0, 300000, 5)
-    os.environ[knob[0]] = knob[1]
-    try:
-        b = grid.run(p, 0, 300000, 5)
-    finally:
-        os.environ.pop(knob[0])
+    la = grid.last_launch()
+    grid.set_tuning(**{knob[0]: knob[1]})
+    b = grid.run(p, 0, 300000, 5)
+    assert grid.last_launch() != la
     grid.close()
     np.testing.assert_allclose(a.det[:2], b.det[:2], rtol=1e-9, atol=1e-300)
     np.testing.assert_array_equal(a.det[2], b.det[2])

@@ -61,9 +61,14 @@ def _run(lib, case):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
+@pytest.mark.parametrize("build", ["debug", "nbf_debug"])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_debug_build_list_invariants(require_gpu, case):
-    dbg = os.path.join(ROOT, "artes_amd", "lib", "libartes_hip_debug.so")
+def test_debug_build_list_invariants(require_gpu, case, build):
+    """Both checked builds -- the shipping evaluation order and the nearest-pending-bound-first
+    order (ARTES_NBF), which shares the pending-bit logic -- over the stress
+    schedules (environment tuning: the debug builds are development builds), against the
+    production library on its default schedule."""
+    dbg = os.path.join(ROOT, "artes_amd", "lib", f"libartes_hip_{build}.so")
     rel = os.path.join(ROOT, "artes_amd", "lib", "libartes_hip.so")
     assert os.path.exists(dbg), "build() makes the ARTES_DEBUG library"
     d = _run(dbg, CASES[case])

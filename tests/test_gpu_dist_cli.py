@@ -85,3 +85,68 @@ def test_cli_two_ranks_on_hip_engine_equals_one(tmp_path, require_gpu):
         # their sigmas) against Stokes I's scale, since Q and U sums cancel towards zero
         np.testing.assert_array_equal(p2[:, 0], p1[:, 0])
         np.testing.assert_allclose(p2[:, 1:], p1[:, 1:], rtol=1e-9, atol=1e-11 * np.abs(p1[:, 1]).max())
+
+
+RCCL_WORKER = r'''
+import json, sys
+sys.path.insert(0, {root!r})
+import torch.distributed as tdist
+from artes_amd import dist, runner
+for mode, n in (("imaging_mono", "{n_img}"), ("spectrum", "{n_spec}")):
+    assert runner.run(["atm_" + mode, n, "-o", "rc_" + mode, "-k", "photon:fstop=2d-5", "--seed", "77"],
+                      root={root_dir!r}) == 0
+r = dist.env_rank()
+v = (0x1234ABCD << 32) | 0x0F0F0F0F
+b = dist.broadcast_int(v, r)
+print(json.dumps(dict(backend=tdist.get_backend(), world=tdist.get_world_size(), coll=dist.COLLECTIVES, bcast=b == v)))
+tdist.destroy_process_group()
+'''
+
+
+def test_cli_rccl_one_rank_equals_plain(tmp_path, require_gpu):
+    """The CLI's RCCL reduction path (VERDICT r04 #3): a fresh process with a one-rank `nccl`
+    process group (ARTES_DIST_FORCE=1, ARTES_DIST_BACKEND=nccl, set up before any GPU call)
+    runs ``runner.run`` on imaging_mono and a 3-wavelength spectrum; every engine call's sums
+    then travel through the GPU in ``dist.allreduce_numpy``'s device branch, and
+    ``dist.broadcast_int`` (the clock seed shared across ranks) rides on it.  The output
+    trees equal the plain one-process run's (ARTES.f90:534-546, 957-975)."""
+    import json
+
+    for mode in ("imaging_mono", "spectrum"):
+        d = tmp_path / "input" / f"atm_{mode}"
+        d.mkdir(parents=True)
+        (d / "artes.in").write_text(ARTES_IN.format(mode=mode))
+        kw = dict(nr=8, ntheta=6, nphi=8) if mode == "imaging_mono" else dict(nr=8, wavelength=(0.5, 0.7, 0.9))
+        atmosphere.write_atmosphere_fits(str(d / "atmosphere.fits"),
+                                         synthetic.make_config("ray3d" if mode == "imaging_mono" else "hg", **kw))
+    script = tmp_path / "rccl_worker.py"
+    script.write_text(RCCL_WORKER.format(root=ROOT, root_dir=str(tmp_path), n_img=N_IMG, n_spec=N_SPEC))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29657", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0",
+               ARTES_DIST_FORCE="1", ARTES_DIST_BACKEND="nccl")
+    env.pop("ARTES_LIB_PATH", None)
+    out = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+    info = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert info["backend"] == "nccl" and info["world"] == 1 and info["bcast"], info
+    # one device all-reduce per engine call: 1 imaging call + 3 wavelengths, + the broadcast
+    assert info["coll"]["device"] == 1 + 3 + 1 and info["coll"]["host"] == 0, info
+
+    for mode in ("imaging_mono", "spectrum"):
+        n = N_IMG if mode == "imaging_mono" else N_SPEC
+        assert runner.run([f"atm_{mode}", n, "-o", f"p1_{mode}", "-k", "photon:fstop=2d-5", "--seed", "77"],
+                          root=str(tmp_path)) == 0
+        one, rc = tmp_path / "output" / f"p1_{mode}", tmp_path / "output" / f"rc_{mode}"
+        assert _files(one) == _files(rc)
+        for f in EXACT:
+            if (one / f).exists():
+                assert (one / f).read_bytes() == (rc / f).read_bytes(), f
+        if mode == "imaging_mono":
+            s1, s2 = (fitsio.read(x / "output" / "stokes.fits")[0].data for x in (one, rc))
+            assert s1[0].sum() > 0
+            np.testing.assert_allclose(s2, s1, rtol=1e-11, atol=1e-11 * np.abs(s1).max())
+            p1, p2 = _rows(one / "output/photometry.dat"), _rows(rc / "output/photometry.dat")
+        else:
+            p1, p2 = _rows(one / "output/spectrum.dat"), _rows(rc / "output/spectrum.dat")
+            assert p1.shape == (3, 5)
+        np.testing.assert_array_equal(p2[:, 0], p1[:, 0])
+        np.testing.assert_allclose(p2[:, 1:], p1[:, 1:], rtol=1e-9, atol=1e-11 * np.abs(p1[:, 1]).max())

@@ -22,36 +22,21 @@ def _setup(name="ray3d", **spec):
     return atm, grid, p
 
 
-class _env:
-    def __init__(self, **kv):
-        self.kv = kv
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update(self.kv)
-
-    def __exit__(self, *a):
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
 def test_event_and_persistent_engines_agree(require_gpu):
     atm, grid, p = _setup(nr=8, ntheta=8, nphi=8)
     ev = grid.trace(p, 0, 20000, 4242)
-    with _env(ARTES_ENGINE="persistent"):
-        pe = grid.trace(p, 0, 20000, 4242)
+    assert grid.last_launch().startswith("k_trace<1,0,4,0,8>")
+    grid.set_tuning(engine="persistent")
+    pe = grid.trace(p, 0, 20000, 4242)
+    assert grid.last_launch() == "persistent"
     same = stats.records_agree(ev, pe)
     assert same.mean() >= 0.999
 
 
-@pytest.mark.parametrize("knobs", [dict(ARTES_POOL="5000"), dict(ARTES_REFILL="1", ARTES_STATIC="0"),
-                                   dict(ARTES_REFILL="64", ARTES_STATIC="64"), dict(ARTES_EVENT_LDS="0", ARTES_DET_LDS="0"), dict(ARTES_WPE="3"),
-                                   dict(ARTES_EMIT_FIRST="0"), dict(ARTES_EMIT_FIRST="1", ARTES_POOL="3000"),
-                                   dict(ARTES_BATCH="4", ARTES_BATCH_MIN="24"), dict(ARTES_BATCH="64", ARTES_BATCH_MIN="0"),
-                                   dict(ARTES_EVENT_BLOCK="256")])
+@pytest.mark.parametrize("knobs", [dict(pool=5000), dict(refill=1, static=0), dict(refill=64, static=64),
+                                   dict(event_lds=0, det_lds=0), dict(wpe=3), dict(emit_first=0),
+                                   dict(emit_first=1, pool=3000), dict(batch=4, batch_min=24),
+                                   dict(batch=64, batch_min=1), dict(event_block=256)])
 def test_launch_knobs_do_not_change_results(require_gpu, knobs):
     """Pool size, refill policy, trace-list split, LDS staging, occupancy, the k_event block
     shape and the batching of the forced first interaction only change the schedule: per-packet histories and
@@ -59,9 +44,10 @@ def test_launch_knobs_do_not_change_results(require_gpu, knobs):
     atm, grid, p = _setup("hg")
     base = grid.run(p, 0, 300000, 99)
     grid.close()
-    with _env(**knobs):
-        atm, grid, p = _setup("hg")
-        other = grid.run(p, 0, 300000, 99)
+    atm, grid, p = _setup("hg")
+    grid.set_tuning(**knobs)
+    assert grid.tuning() == knobs
+    other = grid.run(p, 0, 300000, 99)
     np.testing.assert_array_equal(base.counters, other.counters)
     np.testing.assert_allclose(base.det, other.det, rtol=1e-9, atol=1e-300)
     np.testing.assert_allclose(base.totals, other.totals, rtol=1e-9)
@@ -74,13 +60,12 @@ def test_backward_propagation_matches_forward(require_gpu, name, spec):
     per-packet crossing counts are reported as the forward walk's."""
     atm, grid, p = _setup(name, **spec)
     back = grid.trace(p, 0, 20000, 31)
-    with _env(ARTES_BACKWARD="0"):
-        fwd = grid.trace(p, 0, 20000, 31)
+    c_back = grid.run(p, 0, 200000, 8).counter("crossings")
+    grid.set_tuning(backward=0)
+    fwd = grid.trace(p, 0, 20000, 31)
     same = stats.records_agree(back, fwd)
     assert same.mean() >= 0.999
-    with _env(ARTES_BACKWARD="0"):
-        c_fwd = grid.run(p, 0, 200000, 8).counter("crossings")
-    c_back = grid.run(p, 0, 200000, 8).counter("crossings")
+    c_fwd = grid.run(p, 0, 200000, 8).counter("crossings")
     assert c_back == pytest.approx(c_fwd, rel=1e-3)
 
 
@@ -125,8 +110,9 @@ def test_kernel_times_profiling(require_gpu):
     total = sum(ms for ms, _ in kt.values())
     assert total <= grid.last_kernel_ms() * 1.05 + 0.5
     assert grid.kernel_times()["trace"] == (0.0, 0)          # reset after reading
-    with _env(ARTES_ENGINE="persistent"):
-        grid.run(p, 0, 10**5, 1)
+    grid.set_tuning(engine="persistent")
+    grid.run(p, 0, 10**5, 1)
+    grid.set_tuning(engine=None)
     kt = grid.kernel_times()
     assert kt["persistent"][1] == 1 and kt["trace"][1] == 0
 
@@ -178,3 +164,56 @@ def test_bench_line_contract(require_gpu):
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-4
     assert r["events_per_packet"]["crossings"] > 50 and d["errors"] == {}
+
+
+def test_tuning_keys_are_checked(require_gpu):
+    """artes_set_tuning: unknown keys and out-of-range values fail with -22 ("steps"
+    other than 4 / 8 used to map silently to 8); -1 restores a default."""
+    from artes_amd.engine import EngineError
+
+    atm, grid, p = _setup(nr=8, ntheta=8, nphi=8)
+    for bad in (dict(steps=2), dict(steps=6), dict(batch_min=0), dict(event_block=512), dict(wpe=5), dict(nosuchkey=1)):
+        with pytest.raises(EngineError):
+            grid.set_tuning(**bad)
+    assert grid.tuning() == {}
+    grid.set_tuning(steps=4)
+    grid.run(p, 0, 10**4, 1)
+    assert grid.last_launch().startswith("k_trace<1,0,4,0,4>")
+    grid.set_tuning(steps=None)
+    assert grid.tuning() == {}
+    grid.run(p, 0, 10**4, 1)
+    assert grid.last_launch().startswith("k_trace<1,0,4,0,4>")   # (512 cells: a coarse grid)
+    _, g1, p1 = _setup("hg")
+    with pytest.raises(EngineError, match="radial-only"):
+        g1.set_tuning(steps=4)
+
+
+def test_production_library_ignores_environment(require_gpu):
+    """The production library reads no ARTES_* variable: a child process with
+    ARTES_ENGINE=persistent ARTES_STEPS=4 ARTES_POOL=3000 transports exactly what a clean one
+    does, with the default kernels."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    script = (
+        "import json, sys; sys.path.insert(0, %r)\n"
+        "from artes_amd import driver, synthetic\n"
+        "from artes_amd.engine import Grid\n"
+        "atm = synthetic.make_config('ray3d', nr=16, ntheta=16, nphi=16)\n"
+        "cfg = driver.default_config(); det = driver.detector_geometry(cfg, float(atm['radial'][-1]))\n"
+        "g = Grid(atm, 0); p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0))\n"
+        "r = g.run(p, 0, 100000, 3)\n"
+        "print(json.dumps(dict(l=g.last_launch(), c=[int(x) for x in r.counters], d=float(r.det[0].sum()), t=g.tuning())))\n"
+    ) % ROOT
+    outs = []
+    for extra in ({}, dict(ARTES_ENGINE="persistent", ARTES_STEPS="4", ARTES_POOL="3000", ARTES_REFILL="1")):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("ARTES_")}
+        env.update(extra)
+        out = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+        assert out.returncode == 0, out.stderr[-2000:]
+        outs.append(json.loads(out.stdout.strip().splitlines()[-1]))
+    assert outs[0] == outs[1]
+    assert outs[0]["l"] == "k_trace<1,0,4,0,8> k_event<1,1,0,768,0>" and outs[0]["t"] == {}

@@ -28,6 +28,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _tuning  # noqa: E402
 from artes_amd import driver, synthetic  # noqa: E402
 from artes_amd.engine import Grid  # noqa: E402
 
@@ -83,6 +85,7 @@ def main():
         wl = tuple(np.round(np.linspace(0.45, 0.95, 50), 6))
         atm = synthetic.make_cloudy(os.path.join(tmp, "input", "cloudy50"), wavelength=wl)
         grid = Grid(atm, device=0)
+        _tuning.apply(grid)   # ARTES_* of the environment (artes_set_tuning)
         res = {"config": "BASELINE configs[3]: gas + Mie cloud, 16x6x6 (r,theta,phi), 50 wavelengths 0.45-0.95 um, "
                          "star source, 1-pixel detector",
                "distinct_matrices": grid.num_matrices(), "packets_per_call": n}
@@ -108,6 +111,7 @@ def main():
         fx = os.path.join(ROOT, "tests", "golden", "molecular", "self_luminous_100wl.npz")
         atm = synthetic.make_self_luminous(os.path.join(tmp, "input", "sl"), fx)
         grid = Grid(atm, device=0)
+        _tuning.apply(grid)   # ARTES_* of the environment (artes_set_tuning)
         cfg = driver.default_config()
         cfg.apply("photon:source", "planet")
         cfg.apply("detector:type", "spectrum")

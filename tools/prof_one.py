@@ -3,6 +3,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _tuning  # noqa: E402
 from artes_amd import driver, synthetic  # noqa: E402
 from artes_amd.engine import Grid  # noqa: E402
 
@@ -17,6 +19,7 @@ else:
     atm = synthetic.make_config(name, share_matrix=True)
 det = driver.detector_geometry(cfg, atm["radial"][-1])
 g = Grid(atm, 0)
+_tuning.apply(g)   # ARTES_* of the environment (artes_set_tuning)
 p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0), packet_moments=False)
 w = g.run(p, 0, 10**5, 1)
 r = g.run(p, 0, n, 2024)

@@ -9,6 +9,9 @@ import numpy as np  # noqa: E402
 from artes_amd import driver, stats, synthetic  # noqa: E402
 from artes_amd.engine import Grid  # noqa: E402
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _tuning  # noqa: E402
+
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 5 * 10**7
 variants = [dict(kv.split("=", 1) for kv in v.split(",")) if v else {} for v in (sys.argv[2:] or [""])]
 cfg = driver.default_config()
@@ -19,6 +22,7 @@ for name in ("ray3d", "hg", "iso"):
     atm = synthetic.make_config(name, share_matrix=True)
     det = driver.detector_geometry(cfg, atm["radial"][-1])
     g = Grid(atm, 0)
+    _tuning.apply(g)   # ARTES_* of the environment (artes_set_tuning)
     p = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0))
     if check:
         rec = g.trace(p, 0, 20000, 777)
@@ -29,6 +33,7 @@ for name in ("ray3d", "hg", "iso"):
     for env in variants:
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
+        tv = _tuning.apply(g, env)
         # QP_MOMENTS=0: production configuration without packet-level moments
         pv = driver.run_params(cfg, det, 0, cell_depth=g.cell_depth(0),
                                packet_moments=os.environ.get("QP_MOMENTS", "1") == "1")
@@ -44,4 +49,7 @@ for name in ("ray3d", "hg", "iso"):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+        if tv:
+            g.set_tuning(**{k: None for k in tv})
+            _tuning.apply(g)
     g.close()
