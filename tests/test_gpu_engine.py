@@ -25,7 +25,7 @@ def _setup(name="ray3d", **spec):
 def test_event_and_persistent_engines_agree(require_gpu):
     atm, grid, p = _setup(nr=8, ntheta=8, nphi=8)
     ev = grid.trace(p, 0, 20000, 4242)
-    assert grid.last_launch().startswith("k_trace<1,0,4,0,8>")
+    assert grid.last_launch().startswith("k_trace<1,0,4,0,4>")   # (512 cells: a coarse grid, 4 steps)
     grid.set_tuning(engine="persistent")
     pe = grid.trace(p, 0, 20000, 4242)
     assert grid.last_launch() == "persistent"
