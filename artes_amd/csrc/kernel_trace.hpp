@@ -37,11 +37,6 @@ static constexpr bool TREL_ON = false;   // A/B builds: the radial family re-sol
 #else
 static constexpr bool TREL_ON = true;    // the radial family trace-relative (radial_tr)
 #endif
-#ifdef ARTES_NO_TREL_PHI
-static constexpr bool TREL_PHI = false;  // A/B builds: phi in the batched per-step form with theta
-#else
-static constexpr bool TREL_PHI = true;   // the phi family trace-relative too (phi_tr), outside the batched theta form
-#endif
 // ARTES_DEBUG_TIMING (development build, tools/time_regions.py): per wave, the shader-clock
 // cycles spent in each region of the k_trace loop, summed into the error slots 0-7 (the
 // run's error codes are void then)
@@ -93,6 +88,18 @@ __device__ __forceinline__ double fast_sqrt(double x) {
 // trans-use hazard wait.)
 __device__ __forceinline__ double fast_sqrt0(double x, double cap = 1.e300) {
     const double y = fmin(__builtin_amdgcn_rsq(x), cap);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-g, h, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    const double d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+
+// sqrt(x) to ~1 ulp for x > 0; NaN for x <= 0 (0 * rsq(0) = 0 * inf).  For the radial roots,
+// where a zero or negative discriminant gives no crossing and NaN roots fail every test.
+__device__ __forceinline__ double fast_sqrt_nan0(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
     double g = x * y, h = 0.5 * y;
     const double r = fma(-g, h, 0.5);
     g = fma(g, r, g);
@@ -193,6 +200,11 @@ __device__ __forceinline__ double min_nonan(double a, double b) {
 }
 
 constexpr double INF = __builtin_inf();
+
+// k_trace's `parked` codes: 1 (3 after a cell error) the forced first interaction waits, 4 the
+// interaction waits; PK_END and its bits (trace-relative kernels): a trace end found in a step,
+// resolved at the end of the iteration
+enum : int { PK_END = 8, PK_EXIT = 16, PK_SURF = 32, PK_ERR31 = 64, PK_RUNAWAY = 128, PK_ERR = 256 };
 
 // x if valid, else a NaN: only the high word is selected (one v_cndmask instead of two
 // for a double select).  min_nonan ignores the NaN, and every compare with it is false, so
@@ -447,7 +459,11 @@ __device__ __forceinline__ double radial_tr(const TraceTabs& T, double b0, doubl
     const bool ch = in_ok == alt;   // outer face: !in_ok, turned by alt
     const double r = ch ? rr.y : rr.x;
     const double disc = (r - pm) * (r + pm);
-    const double sq = fast_sqrt0(disc, K.cap);
+    // (no cap on the rsq seed: a zero discriminant -- a double root, which gives no crossing --
+    // then yields NaN roots, and a negative one NaN as well; every comparison of a NaN is false,
+    // so both roots are rejected exactly as by the reference's rules; two instructions and the
+    // discriminant's test fewer than fast_sqrt0)
+    const double sq = fast_sqrt_nan0(disc);
     const double sA = -b0 - sq, sB = sq - b0;
     const double dA = sA - t, dB = sB - t;
     const bool same = onr & (fi == cr + (ch ? 1 : 0));
@@ -455,7 +471,7 @@ __device__ __forceinline__ double radial_tr(const TraceTabs& T, double b0, doubl
     // (equal roots give none: with dA == dB both pass or fail their tests together, so the
     // rule is one more term of each AND chain; the chains stay lane masks, and the nearer
     // valid root is one min -- sA <= sB -- instead of a branch)
-    const bool ok = (disc >= 0.0) & !(same & !ch) & (dA != dB);
+    const bool ok = !(same & !ch) & (dA != dB);
     const bool vA = ok & (dA > tmin) & (dA < K.huge), vB = ok & (dB > tmin) & (dB < K.huge);
     outer = ch;
     return min_nonan(or_nan(vA, sA), or_nan(vB, sB));
@@ -840,6 +856,28 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         pend = 0;
     };
 
+    // The evaluated family's entry is exact now: clear ITS pending bit (fam is always a pending
+    // family, so the xor clears it; two instructions, as `pending & (pending - 1)`).  (The
+    // round-2 "nearest bound first" variant evaluated a family other than the lowest pending one
+    // but kept `pending &= pending - 1`, which clears the LOWEST bit: that family's bound was
+    // then taken for an exact distance, the lane stepped onto it as onto a face, and next_cell
+    // walked the cell indices out of range -- the illegal access of that round, DESIGN.md §4;
+    // ARTES_DEBUG counts such a clear as ARTES_ERR_PENDING.  The trace-relative kernels now
+    // evaluate the nearest pending bound first, with this clear.)
+    auto clear_pending = [&](int fam, bool retry) __attribute__((always_inline)) {
+#ifdef ARTES_DEBUG
+        const int pending_before = pending;
+#endif
+#ifdef ARTES_OLD_CLEAR
+        if (!retry) pending &= pending - 1;   // (development build: the round-2 clear)
+#else
+        if (!retry) pending ^= 1 << fam;
+#endif
+#ifdef ARTES_DEBUG
+        if (!retry && (pending_before & ~pending) != (1 << fam)) log_err(R, ARTES_ERR_PENDING);
+#endif
+    };
+
     // watchdog: a wave runs ~1e4 iterations per launch at the largest pool; a schedule bug
     // must not leave waves spinning on the device (the run then fails with error 57)
     unsigned int iters_left = 1u << 24;
@@ -991,141 +1029,186 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         // ends, parks or waits for a theta batch sits out the rest of the iteration (DESIGN.md
         // §4, "Several steps per iteration").  (A compile-time count: a runtime one, a scalar
         // compare per copy, cost ray3d 3 %.)
+        // The evaluation and the step, NREP times per iteration (unrolled): the iteration's
+        // wave-level blocks -- parked-lane ballots and blocks, refill check and refill,
+        // chain-end stores, queue flushes, loop head -- run once per NREP steps.  A lane that
+        // ends or parks sits out the rest of the iteration ("Several steps per
+        // iteration").  (A compile-time count: a runtime one, a scalar compare per copy, cost
+        // ray3d 3 %.)
 #pragma unroll
         for (int rep = 0; rep < NREP; rep++) {
         TM_TICK(t_rep);   // (timing build: the evaluation is timed from each step's start)
         if (have && !parked && !end) {
             const double k = kext;
-            // ------------------------------------------- evaluate one face family
-#ifdef ARTES_NBF
-            // development variant: the pending family with the nearest bound first
-            int fam = 0;
-            if constexpr (G3D) {
-                const double b0 = (pending & 1) ? e0 : INF, b1 = (pending & 2) ? e1 : INF, b2 = (pending & 4) ? e2 : INF;
-                fam = (b0 <= b1 && b0 <= b2) ? 0 : (b1 <= b2 ? 1 : 2);
-                fam = ((pending >> fam) & 1) ? fam : __builtin_ctz(pending);
-            }
-#else
-            const int fam = G3D ? __builtin_ctz(pending) : 0;
-#endif
-            const int pout = G3D ? ((tcp + 1 == G.nphi) ? 0 : tcp + 1) : 0;
-            // (TREL: theta / phi evaluations batched -- a lane that needs one waits, without
-            // stepping, until R.gbatch lanes of the wave need one or few lanes still step)
-            bool run_eval = true;
+            // the nearest entry (TREL: a trace parameter) and its family; its distance from the
+            // current point; whether the lane steps
+            double best_abs, best;
+            int w;
+            bool fast, do_step;
             if constexpr (TREL) {
-                // (both ballots outside any short-circuit: under `||` the second one would count
-                // only the lanes that reach it)
-                const unsigned long long gm = __ballot(TREL_PHI ? fam == 1 : fam != 0), act = __ballot(true);
-                if (gm) {
-                    const int ng = __popcll(gm);
-                    const bool go = ng >= R.gbatch || __popcll(act) - ng < R.batch_min || exhausted;
-                    run_eval = fam == 0 || (TREL_PHI && fam == 2) || go;
-                }
-            }
-            if (run_eval) {
-            bool outer;
-            // the face the family can cross next; the other one if that has no crossing
-            // (`alt`, bit 4 + fam of `sides`: evaluated in this lane's next iteration).  Both
-            // faces on an oblate grid: there the star's packets start inside the atmosphere's
-            // outer surface (the reference emits them on the unscaled sphere), a position its
-            // cell does not contain, where the nearest crossing is not the one the direction
-            // points to
-            double dm;
-            bool retry = false;
-            if constexpr (OBL || TWOFACE) {
-                dm = family_eval<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, outer);
-            } else {
-                const bool alt = (sides >> (4 + fam)) & 1;
-                if constexpr (TREL) {
-                    if (fam == 0) {
-                        dm = radial_tr(T, b0, pm, tpar, tft, tfi, tcr, alt, K, outer);
-                    } else if (TREL_PHI && fam == 2) {
-                        dm = phi_tr(T, tx, ty, nx, ny, tpar, tft, tfi, tcp, pout, K, outer);
-                    } else {   // theta / phi (~0.1-0.4 % of crossings): from the current point
-                        TM_TICK(ta);
-                        const double qx = fma(tpar, nx, tx), qy = fma(tpar, ny, ty), qz = fma(tpar, nz, tz);
-#ifdef ARTES_THETA2   // (development build: both theta faces at once, no other-face retry)
-                        dm = tpar + family_eval<G3D, OBL>(G, T, fam, qx, qy, qz, nx, ny, nz, dir_axy(ax2, by2, nx, ny),
-                                                          cz2 * nz * nz, tft, tfi, tcr, tct, tcp, pout, -qz * fast_rcp(nz), outer);
-#else
-                        dm = tpar + family_eval1<G3D, OBL, true>(G, T, fam, qx, qy, qz, nx, ny, nz, dir_axy(ax2, by2, nx, ny),
-                                                                 cz2 * nz * nz, tft, tfi, tcr, tct, tcp, pout, -qz * fast_rcp(nz), alt, K,
-                                                                 outer);
-#endif
-                        TM_TICK(tb);
-                        TM_ADD(5, tb - ta);
-                    }
-                } else {
-                    dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
-                }
-                retry = (fam != 2) & !alt & !(dm < K.inf);
-#ifdef ARTES_THETA2
-                if constexpr (TREL) retry = retry & (fam == 0);
-#endif
-            }
-            // (the other face is still to come: no bound.  Only the high word is cleared: the
-            // entry is then 0 or a positive denormal, below any step, so the family stays the
-            // nearest pending one exactly as with 0; TREL: the current trace parameter)
-            if constexpr (TREL) dm = retry ? tpar : dm;
-            else if constexpr (LAZY) dm = __hiloint2double(retry ? 0 : __double2hiint(dm), __double2loint(dm));
-            if constexpr (G3D) {
-                e0 = fam == 0 ? dm : e0;
-                e1 = fam == 1 ? dm : e1;
-                e2 = fam == 2 ? dm : e2;
-                sides = (sides & ~(0x11 << fam)) | (((outer ? 1 : 0) | (retry ? 16 : 0)) << fam);
-            } else {
-                e0 = dm;
-                sides = (outer ? 1 : 0) | ((retry ? 1 : 0) << 4);
-            }
-            // the evaluated family's entry is exact now: clear ITS bit (fam is always a pending
-            // family, so the xor clears it; two instructions, as `pending & (pending - 1)`).
-            // (The round-2 "nearest bound first" variant evaluated a family other than the lowest
-            // pending one but kept `pending &= pending - 1`, which clears the LOWEST bit: that
-            // family's bound was then taken for an exact distance, the lane stepped onto it as
-            // onto a face, and next_cell walked the cell indices out of range -- the illegal
-            // access of that round; ARTES_DEBUG counts such a clear as
-            // ARTES_ERR_PENDING.)
-#ifdef ARTES_DEBUG
-            const int pending_before = pending;
-#endif
-#ifdef ARTES_OLD_CLEAR
-            if (!retry) pending &= pending - 1;   // (development build: the round-2 clear)
-#else
-            if (!retry) pending ^= 1 << fam;
-#endif
-#ifdef ARTES_DEBUG
-            if (!retry && (pending_before & ~pending) != (1 << fam)) log_err(R, ARTES_ERR_PENDING);
-#endif
+                // A. The radial family, whenever its entry is not exact (pending bit 0): the last
+                // step crossed a sphere (99.9 % of all crossings on the bench grid), a trace starts,
+                // or the chosen sphere had no crossing (`alt`: the other one).  No per-lane choice
+                // of the family to evaluate: every lane that evaluates at all evaluates this one.
+                if (pending & 1) {
+                    const bool alt = (sides >> 4) & 1;
+                    bool outer;
+                    const double dm = radial_tr(T, b0, pm, tpar, tft, tfi, tcr, alt, K, outer);
+                    const bool retry = !alt & !(dm < K.inf);
+                    // (the other face is still to come: the entry is the current trace parameter,
+                    // the nearest one, and the bit stays pending)
+                    e0 = retry ? tpar : dm;
+                    sides = (sides & ~0x11) | (outer ? 1 : 0) | (retry ? 16 : 0);
+                    clear_pending(0, retry);
 #ifdef ARTES_DEBUG_LANES
-            dbg_r = retry; dbg_u = true;   // (evaluated; lanes that also step are subtracted below)
-            {
-                const unsigned long long bf = __ballot(fam != 0), bp = __ballot(fam == 2);
-                dbg_f12 += __popcll(bf);
-                dbg_anyf12 += bf != 0;
-                dbg_f2 += __popcll(bp);
-                dbg_anyf2 += bp != 0;
-            }
+                    dbg_r = retry; dbg_u = true;
 #endif
-            }   // run_eval
-            TM_TICK(tev);
-            TM_ADD(2, tev - t_rep);
-            // ---------------------------------------------------- trace step
-            // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
-            // The nearest distance of the three is the reference's choice whenever it
-            // exceeds 1e-9 m (then all of them do); the two-pass rule runs only when it
-            // does not (a crossing at a corner of two families) or nothing is ahead.
-            // (NaN: no crossing; ties go to the lower family, as the reference's order.)
-            // With pending families (bounds), only an exact nearest entry beyond 1e-9 m steps.
-            // (TREL: the entries are trace parameters; best_abs the nearest one, best its distance)
-            double best_abs = e0;
-            int w = 0;
-            if constexpr (G3D) {
-                best_abs = min_nonan(min_nonan(e0, e1), e2);
-                w = e0 == best_abs ? 0 : (e1 == best_abs ? 1 : 2);
+                }
+                // B. The choice: the nearest of the three entries.  A lane steps unless a pending
+                // family blocks it -- its bound is the nearest entry, or some family is pending and
+                // nothing lies beyond 1e-9 m -- (the reference's choice whenever it steps: a pending
+                // family's candidate lies at least as far as its bound, DESIGN.md §4 "Lazy set-up")
+                best_abs = e0;
+                w = 0;
+                if constexpr (G3D) {
+                    best_abs = min_nonan(min_nonan(e0, e1), e2);
+                    w = e0 == best_abs ? 0 : (e1 == best_abs ? 1 : 2);
+                }
+                best = best_abs - tpar;
+                fast = best > K.step_min && best < K.inf;
+                const bool blocked = ((pending >> w) & 1) | (!fast & (pending != 0));
+                // C. Theta / phi (3D grids): the blocking family when it is one of them (a lane whose
+                // radial entry is still pending runs A again in its next step) -- the nearest pending
+                // bound first (w), or the lowest pending family when nothing lies beyond 1e-9 m.
+                // Theta evaluations (the quadratic from the current point) are batched: a lane that
+                // needs one waits until R.gbatch lanes of the wave do, or few lanes still step.
+                if constexpr (G3D) {
+                    const bool tp = blocked && !(pending & 1);
+                    const unsigned long long act = __ballot(true);
+                    if (__ballot(tp)) {   // (a wave-uniform test first: ~10 % of the steps need this)
+                    const int fam = fast ? w : __builtin_ctz(pending & 6);
+                    // (both ballots outside any short-circuit: under `||` the second one would count
+                    // only the lanes that reach it)
+                    const unsigned long long gm = __ballot(tp && fam == 1), pm2 = __ballot(tp && fam == 2);
+                    {
+                        bool run = tp && fam == 2;
+                        if (gm) {
+                            const int ng = __popcll(gm);
+                            const bool go = ng >= R.gbatch || __popcll(act) - ng < R.batch_min || exhausted;
+                            run = run || (tp && fam == 1 && go);
+                        }
+                        if (run) {
+                            const int pout = (tcp + 1 == G.nphi) ? 0 : tcp + 1;
+                            const bool alt = (sides >> (4 + fam)) & 1;
+                            bool outer;
+                            double dm;
+                            if (fam == 2) {
+                                dm = phi_tr(T, tx, ty, nx, ny, tpar, tft, tfi, tcp, pout, K, outer);
+                            } else {   // theta (~0.1-0.4 % of crossings): from the current point
+                                TM_TICK(ta);
+                                const double qx = fma(tpar, nx, tx), qy = fma(tpar, ny, ty), qz = fma(tpar, nz, tz);
+                                dm = tpar + family_eval1<G3D, OBL, true>(G, T, fam, qx, qy, qz, nx, ny, nz, dir_axy(ax2, by2, nx, ny),
+                                                                         cz2 * nz * nz, tft, tfi, tcr, tct, tcp, pout, -qz * fast_rcp(nz),
+                                                                         alt, K, outer);
+                                TM_TICK(tb);
+                                TM_ADD(5, tb - ta);
+                            }
+                            const bool retry = (fam == 1) & !alt & !(dm < K.inf);
+                            dm = retry ? tpar : dm;
+                            e1 = fam == 1 ? dm : e1;
+                            e2 = fam == 2 ? dm : e2;
+                            sides = (sides & ~(0x11 << fam)) | (((outer ? 1 : 0) | (retry ? 16 : 0)) << fam);
+                            clear_pending(fam, retry);
+#ifdef ARTES_DEBUG_LANES
+                            dbg_r = retry; dbg_u = true;
+#endif
+                        }
+#ifdef ARTES_DEBUG_LANES
+                        dbg_f12 += __popcll(gm | pm2);
+                        dbg_anyf12 += 1;
+                        dbg_f2 += __popcll(pm2);
+                        dbg_anyf2 += pm2 != 0;
+#endif
+                    }
+                    }   // any tp
+                }
+                TM_TICK(tev);
+                TM_ADD(2, tev - t_rep);
+                // D. The step below (a lane that evaluated theta / phi above steps in its next one)
+                do_step = !blocked;
+            } else {
+                // ------------------------------------------- evaluate one face family
+    #ifdef ARTES_NBF
+                // development variant: the pending family with the nearest bound first
+                int fam = 0;
+                if constexpr (G3D) {
+                    const double b0 = (pending & 1) ? e0 : INF, b1 = (pending & 2) ? e1 : INF, b2 = (pending & 4) ? e2 : INF;
+                    fam = (b0 <= b1 && b0 <= b2) ? 0 : (b1 <= b2 ? 1 : 2);
+                    fam = ((pending >> fam) & 1) ? fam : __builtin_ctz(pending);
+                }
+    #else
+                const int fam = G3D ? __builtin_ctz(pending) : 0;
+    #endif
+                const int pout = G3D ? ((tcp + 1 == G.nphi) ? 0 : tcp + 1) : 0;
+                bool outer;
+                // the face the family can cross next; the other one if that has no crossing
+                // (`alt`, bit 4 + fam of `sides`: evaluated in this lane's next iteration).  Both
+                // faces on an oblate grid: there the star's packets start inside the atmosphere's
+                // outer surface (the reference emits them on the unscaled sphere), a position its
+                // cell does not contain, where the nearest crossing is not the one the direction
+                // points to
+                double dm;
+                bool retry = false;
+                if constexpr (OBL || TWOFACE) {
+                    dm = family_eval<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, outer);
+                } else {
+                    const bool alt = (sides >> (4 + fam)) & 1;
+                    dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
+                    retry = (fam != 2) & !alt & !(dm < K.inf);
+                }
+                // (the other face is still to come: no bound.  Only the high word is cleared: the
+                // entry is then 0 or a positive denormal, below any step, so the family stays the
+                // nearest pending one exactly as with 0)
+                if constexpr (LAZY) dm = __hiloint2double(retry ? 0 : __double2hiint(dm), __double2loint(dm));
+                if constexpr (G3D) {
+                    e0 = fam == 0 ? dm : e0;
+                    e1 = fam == 1 ? dm : e1;
+                    e2 = fam == 2 ? dm : e2;
+                    sides = (sides & ~(0x11 << fam)) | (((outer ? 1 : 0) | (retry ? 16 : 0)) << fam);
+                } else {
+                    e0 = dm;
+                    sides = (outer ? 1 : 0) | ((retry ? 1 : 0) << 4);
+                }
+                // the evaluated family's entry is exact now: clear ITS bit (see clear_pending)
+                clear_pending(fam, retry);
+    #ifdef ARTES_DEBUG_LANES
+                dbg_r = retry; dbg_u = true;   // (evaluated; lanes that also step are subtracted below)
+    #endif
+                TM_TICK(tev);
+                TM_ADD(2, tev - t_rep);
+                // ---------------------------------------------------- trace step
+                // nearest face, 'large' then 'small' solutions (ARTES.f90:3358-3418)
+                // The nearest distance of the three is the reference's choice whenever it
+                // exceeds 1e-9 m (then all of them do); the two-pass rule runs only when it
+                // does not (a crossing at a corner of two families) or nothing is ahead.
+                // (NaN: no crossing; ties go to the lower family, as the reference's order.)
+                // With pending families (bounds), only an exact nearest entry beyond 1e-9 m steps.
+                // (TREL: the entries are trace parameters; best_abs the nearest one, best its distance)
+                best_abs = e0;
+                w = 0;
+                if constexpr (G3D) {
+                    best_abs = min_nonan(min_nonan(e0, e1), e2);
+                    w = e0 == best_abs ? 0 : (e1 == best_abs ? 1 : 2);
+                }
+                best = best_abs;
+                fast = best > K.step_min && best < K.inf;
+                do_step = pending == 0 || (LAZY && fast && !((pending >> w) & 1));
             }
-            double best = TREL ? best_abs - tpar : best_abs;
-            const bool fast = best > K.step_min && best < K.inf;
-            if (pending == 0 || (LAZY && fast && !((pending >> w) & 1))) {
+            // ---------------------------------------------------- the step
+            // From the nearest entry best_abs of family w: the reference's two-pass choice when
+            // that is not beyond 1e-9 m (ARTES.f90:3358-3418), next_cell (2671-2798), the
+            // optical-depth sum and the trace ends (625-778, 848-941, 4739-4761)
+            if (do_step) {
                 if (!fast) {   // rare (every family exact here)
                     const double r0 = TREL ? e0 - tpar : e0, r1 = TREL ? e1 - tpar : e1, r2 = TREL ? e2 - tpar : e2;
                     const double t0 = or_nan(r0 > 1.e-9, r0);
@@ -1165,7 +1248,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
                 const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
                 bool err = err31 | ((tft == 1) & (tfi == G.cell_depth) & surf);
-#ifdef ARTES_DEBUG
+    #ifdef ARTES_DEBUG
                 {   // the new index of the crossed family must name a cell unless the trace leaves
                     // the grid or reaches the surface (ARTES_ERR_CELL: the packet is dropped before
                     // its out-of-range kappa read, and the run fails)
@@ -1175,7 +1258,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         err = true;
                     }
                 }
-#endif
+    #endif
                 // (the error codes are logged on the chain-end paths below: every error stops)
                 auto log_step_err = [&]() {
                     if (runaway) log_err(R, ARTES_ERR_RUNAWAY);
@@ -1186,91 +1269,180 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 const bool prop = (mode == S_PROP);
                 const bool hit = prop && tacc + tau_cell > ttgt;
                 const bool stop = err || exit || surf || hit;
-#ifdef ARTES_DEBUG_LANES
+    #ifdef ARTES_DEBUG_LANES
                 dbg_s = stop; dbg_h = prop && hit && !err; dbg_m = !stop; dbg_u = false;
-#endif
+    #endif
                 if constexpr (FLOW) {
                     if (prop && !err && !hit) {   // the segment to the face (ARTES.f90:728-743, 889-904)
                         const int lat = w == 0 ? (side ? 0 : 1) : (w == 1 ? (side ? 2 : 3) : -1);
                         flow_segment(R.flow_g, R.flow_t, cell, tx + best * nx, ty + best * ny, tz + best * nz, nx, ny, nz, best, wI, lat);
                     }
                 }
-                if (!stop) {
-                    tacc += tau_cell;
-                    if constexpr (TREL) {
+                if constexpr (TREL) {
+                    // Every lane that crosses -- a move, or a trace end other than an interaction --
+                    // takes the crossing's optical depth, trace parameter and face; a move also
+                    // takes the new cell.  The trace ends are resolved once per iteration, after the
+                    // steps (below): inside every step their branches ran in ~90 % of the steps for
+                    // ~4 lanes (a lane that stops sits out the iteration's other steps either way).
+                    const bool hitpark = prop & hit & !err;
+                    if (!hitpark) {
+                        tacc += tau_cell;
                         tpar = best_abs;
-                    } else {
-                        tx = fma(best, nx, tx); ty = fma(best, ny, ty); tz = fma(best, nz, tz);
+                        tft = w + 1; tfi = nfi;
                     }
-                    tft = w + 1; tfi = nfi;
-                    if constexpr (G3D) {
-                        tcr = w == 0 ? kn : tcr;
-                        tct = w == 1 ? kn : tct;
-                        tcp = w == 2 ? kn : tcp;
-                        cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
-                        if constexpr (!TREL) { e0 -= best; e1 -= best; e2 -= best; }
-                    } else {
-                        cell += kn - kf;
-                        tcr = kn;
-                    }
-                    load_cell();
-                    pending |= 1 << w;
-                } else if (prop && !err && hit) {
-                    // the interaction in this cell waits, parked, until enough lanes of the
-                    // wave need it (the top of the loop)
-                    parked = 4;
-                } else if (prop) {
-                    if (err) {
-                        log_step_err();
-                        log_err(R, 3);
-                        end = S_END_DROP;
-                    } else if (exit) {                             // left the atmosphere
-                        end = S_END_EXIT;
-                    } else {                                       // reached the surface (ARTES.f90:755-774)
-                        // (xi > albedo: absorbed; a black surface absorbs whatever xi is, and
-                        // an ended packet's RNG state is not used again, so no draw then)
-                        bool absorbed = true;
-                        if (R.surface_albedo > 0.0) absorbed = rng.uni() > R.surface_albedo;
-                        if (absorbed) {
-                            end = S_END_ABS;
+                    if (!stop) {
+                        if constexpr (G3D) {
+                            tcr = w == 0 ? kn : tcr;
+                            tct = w == 1 ? kn : tct;
+                            tcp = w == 2 ? kn : tcp;
+                            cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
                         } else {
-                            // Lambertian reflection: k_event turns the packet at the surface point,
-                            // the propagation then resumes with the optical depth still to go
+                            cell += kn - kf;
+                            tcr = kn;
+                        }
+                        load_cell();
+                        pending |= 1 << w;
+                    } else {
+                        // the interaction waits, parked, until enough lanes of the wave need it (the
+                        // top of the loop); any other end waits for the end of the iteration
+                        parked = hitpark ? 4
+                                         : (PK_END | (exit ? PK_EXIT : 0) | (surf ? PK_SURF : 0) | (err31 ? PK_ERR31 : 0) |
+                                            (runaway ? PK_RUNAWAY : 0) | (err ? PK_ERR : 0));
+                    }
+                } else {
+                    if (!stop) {
+                        tacc += tau_cell;
+                        if constexpr (TREL) {
+                            tpar = best_abs;
+                        } else {
+                            tx = fma(best, nx, tx); ty = fma(best, ny, ty); tz = fma(best, nz, tz);
+                        }
+                        tft = w + 1; tfi = nfi;
+                        if constexpr (G3D) {
+                            tcr = w == 0 ? kn : tcr;
+                            tct = w == 1 ? kn : tct;
+                            tcp = w == 2 ? kn : tcp;
+                            cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
+                            if constexpr (!TREL) { e0 -= best; e1 -= best; e2 -= best; }
+                        } else {
+                            cell += kn - kf;
+                            tcr = kn;
+                        }
+                        load_cell();
+                        pending |= 1 << w;
+                    } else if (prop && !err && hit) {
+                        // the interaction in this cell waits, parked, until enough lanes of the
+                        // wave need it (the top of the loop)
+                        parked = 4;
+                    } else if (prop) {
+                        if (err) {
+                            log_step_err();
+                            log_err(R, 3);
+                            end = S_END_DROP;
+                        } else if (exit) {                             // left the atmosphere
+                            end = S_END_EXIT;
+                        } else {                                       // reached the surface (ARTES.f90:755-774)
+                            // (xi > albedo: absorbed; a black surface absorbs whatever xi is, and
+                            // an ended packet's RNG state is not used again, so no draw then)
+                            bool absorbed = true;
+                            if (R.surface_albedo > 0.0) absorbed = rng.uni() > R.surface_albedo;
+                            if (absorbed) {
+                                end = S_END_ABS;
+                            } else {
+                                // Lambertian reflection: k_event turns the packet at the surface point,
+                                // the propagation then resumes with the optical depth still to go
+                                const double sf = TREL ? best_abs : best;
+                                px = tx + sf * nx; py = ty + sf * ny; pz = tz + sf * nz;
+                                pcell = pack_cell(tcr, tct, tcp);
+                                pface = pack_face(1, G.cell_depth);
+                                ttgt = ttgt - (tacc + tau_cell);
+                                end = S_SURF_HIT;
+                            }
+                        }
+                    } else {   // a first-optical-depth or peel-off trace reached the boundary
+                        tacc += tau_cell;
+                        // error codes of the four traces (ARTES.f90:640, 4743, 4549, 4653)
+                        if (err) {
+                            log_step_err();
+                            log_err(R, mode == S_FIRST ? 2 : mode == S_PEEL ? 43 : mode == S_PEEL_T ? 46 : 42);
+                        }
+                        if (is_peel_trace(mode)) {
+                            const int kind = mode == S_PEEL_T ? 1 : mode == S_PEEL_S ? 2 : 0;
+                            end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0) | (kind << PEEL_KIND_SHIFT);
+                        } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
+                            end = S_END_DROP;
+                        } else {
+                            // the forced first interaction waits (parked, at the chord's far end:
+                            // the position, face and cell of the crossing, for a backward walk)
+                            // until enough lanes of the wave need it (see the top of the loop)
                             const double sf = TREL ? best_abs : best;
-                            px = tx + sf * nx; py = ty + sf * ny; pz = tz + sf * nz;
-                            pcell = pack_cell(tcr, tct, tcp);
-                            pface = pack_face(1, G.cell_depth);
-                            ttgt = ttgt - (tacc + tau_cell);
-                            end = S_SURF_HIT;
+                            tx += sf * nx; ty += sf * ny; tz += sf * nz;
+                            tft = w + 1; tfi = nfi;
+                            parked = err ? 3 : 1;
                         }
                     }
-                } else {   // a first-optical-depth or peel-off trace reached the boundary
-                    tacc += tau_cell;
-                    // error codes of the four traces (ARTES.f90:640, 4743, 4549, 4653)
-                    if (err) {
-                        log_step_err();
-                        log_err(R, mode == S_FIRST ? 2 : mode == S_PEEL ? 43 : mode == S_PEEL_T ? 46 : 42);
-                    }
-                    if (is_peel_trace(mode)) {
-                        const int kind = mode == S_PEEL_T ? 1 : mode == S_PEEL_S ? 2 : 0;
-                        end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0) | (kind << PEEL_KIND_SHIFT);
-                    } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
-                        end = S_END_DROP;
-                    } else {
-                        // the forced first interaction waits (parked, at the chord's far end:
-                        // the position, face and cell of the crossing, for a backward walk)
-                        // until enough lanes of the wave need it (see the top of the loop)
-                        const double sf = TREL ? best_abs : best;
-                        tx += sf * nx; ty += sf * ny; tz += sf * nz;
-                        tft = w + 1; tfi = nfi;
-                        parked = err ? 3 : 1;
-                    }
                 }
-            }   // pending == 0
+            }   // do_step
         }   // have
         }   // rep
         TM_TICK(t3);
         TM_ADD(3, t3 - t2);
+        if constexpr (TREL) {
+            // The trace ends of this iteration's steps (ARTES.f90:640-656, 745-778, 4743-4761), for
+            // every lane that stopped in any of them, once per iteration.  (A surface's albedo draw
+            // moves here from the step: the lane draws nothing in between, so its RNG sequence is
+            // unchanged.)
+            if (__ballot(parked >= PK_END)) {
+                if (parked >= PK_END) {
+                    const int sk = parked;
+                    parked = 0;
+                    const bool exit = (sk & PK_EXIT) != 0, surf = (sk & PK_SURF) != 0, err = (sk & PK_ERR) != 0;
+                    if (err) {
+                        if (sk & PK_RUNAWAY) log_err(R, ARTES_ERR_RUNAWAY);
+                        log_err(R, (sk & PK_ERR31) ? 31 : 34);
+                    }
+                    if (mode == S_PROP) {
+                        if (err) {
+                            log_err(R, 3);
+                            end = S_END_DROP;
+                        } else if (exit) {                             // left the atmosphere
+                            end = S_END_EXIT;
+                        } else {                                       // reached the surface (ARTES.f90:755-774)
+                            // (xi > albedo: absorbed; a black surface absorbs whatever xi is, and
+                            // an ended packet's RNG state is not used again, so no draw then)
+                            bool absorbed = true;
+                            if (R.surface_albedo > 0.0) absorbed = rng.uni() > R.surface_albedo;
+                            if (absorbed) {
+                                end = S_END_ABS;
+                            } else {
+                                // Lambertian reflection: k_event turns the packet at the surface point,
+                                // the propagation then resumes with the optical depth still to go
+                                px = tx + tpar * nx; py = ty + tpar * ny; pz = tz + tpar * nz;
+                                pcell = pack_cell(tcr, tct, tcp);
+                                pface = pack_face(1, G.cell_depth);
+                                ttgt = ttgt - tacc;
+                                end = S_SURF_HIT;
+                            }
+                        }
+                    } else {   // a first-optical-depth or peel-off trace reached the boundary
+                        // error codes of the four traces (ARTES.f90:640, 4743, 4549, 4653)
+                        if (err) log_err(R, mode == S_FIRST ? 2 : mode == S_PEEL ? 43 : mode == S_PEEL_T ? 46 : 42);
+                        if (is_peel_trace(mode)) {
+                            const int kind = mode == S_PEEL_T ? 1 : mode == S_PEEL_S ? 2 : 0;
+                            end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0) | (kind << PEEL_KIND_SHIFT);
+                        } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
+                            end = S_END_DROP;
+                        } else {
+                            // the forced first interaction waits (parked, at the chord's far end: the
+                            // position, face and cell of the crossing, for a backward walk) until
+                            // enough lanes of the wave need it (see the top of the loop)
+                            tx += tpar * nx; ty += tpar * ny; tz += tpar * nz;
+                            parked = err ? 3 : 1;
+                        }
+                    }
+                }
+            }
+        }
         if (end) {   // the chain ends: the record now, the list append below or at the next refill
             c_cross += (uint32_t)(ncross - nc0);
             Slot* rec = S.s + slot;
