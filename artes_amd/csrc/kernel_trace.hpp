@@ -98,12 +98,14 @@ __device__ __forceinline__ double fast_sqrt0(double x, double cap = 1.e300) {
 
 // sqrt(x) to ~1 ulp for x > 0; NaN for x <= 0 (0 * rsq(0) = 0 * inf).  For the radial roots,
 // where a zero or negative discriminant gives no crossing and NaN roots fail every test.
+// (One Goldschmidt step takes the seed's ~2^-23 to ~2^-46; the correction g + d h then needs h
+// only to the seed's accuracy -- its error multiplies d ~ 2^-46 g -- so h is not refined.)
 __device__ __forceinline__ double fast_sqrt_nan0(double x) {
     const double y = __builtin_amdgcn_rsq(x);
-    double g = x * y, h = 0.5 * y;
+    double g = x * y;
+    const double h = 0.5 * y;
     const double r = fma(-g, h, 0.5);
     g = fma(g, r, g);
-    h = fma(h, r, h);
     const double d = fma(-g, g, x);
     return fma(d, h, g);
 }
@@ -455,7 +457,10 @@ __device__ __forceinline__ double radial_tr(const TraceTabs& T, double b0, doubl
                                             bool alt, const TraceK& K, bool& outer) {
     const double2 rr = T.rr[cr];
     const bool onr = ft == 1;
-    const bool in_ok = (t < -b0) & (rr.x >= pm) & !(onr & (fi == cr));
+    // the packet sits on the shell's inner / outer sphere
+    const int df = fi - cr;
+    const bool s_in = onr & (df == 0), s_out = onr & (df == 1);
+    const bool in_ok = (t < -b0) & (rr.x >= pm) & !s_in;
     const bool ch = in_ok == alt;   // outer face: !in_ok, turned by alt
     const double r = ch ? rr.y : rr.x;
     const double disc = (r - pm) * (r + pm);
@@ -466,12 +471,12 @@ __device__ __forceinline__ double radial_tr(const TraceTabs& T, double b0, doubl
     const double sq = fast_sqrt_nan0(disc);
     const double sA = -b0 - sq, sB = sq - b0;
     const double dA = sA - t, dB = sB - t;
-    const bool same = onr & (fi == cr + (ch ? 1 : 0));
-    const double tmin = (same & ch) ? K.tol_same : K.tol;
+    // (re-crossing the sphere the packet sits on: 1e-3 m as the outer face, vetoed as the inner one)
+    const double tmin = (ch & s_out) ? K.tol_same : K.tol;
     // (equal roots give none: with dA == dB both pass or fail their tests together, so the
     // rule is one more term of each AND chain; the chains stay lane masks, and the nearer
     // valid root is one min -- sA <= sB -- instead of a branch)
-    const bool ok = !(same & !ch) & (dA != dB);
+    const bool ok = !(!ch & s_in) & (dA != dB);
     const bool vA = ok & (dA > tmin) & (dA < K.huge), vB = ok & (dB > tmin) & (dB < K.huge);
     outer = ch;
     return min_nonan(or_nan(vA, sA), or_nan(vB, sB));
@@ -598,6 +603,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     unsigned long long dbg_firuns = 0, dbg_filanes = 0, dbg_reflanes = 0, dbg_hruns = 0, dbg_hlanes = 0;
     unsigned long long dbg_f12 = 0, dbg_anyf12 = 0;   // theta / phi evaluations: lanes, iterations with any
     unsigned long long dbg_f2 = 0, dbg_anyf2 = 0;     // the phi ones
+    // per step of the unrolled iteration: lane-steps idle, parked, ended earlier, stepping, blocked
+    unsigned long long dbg_rsteps = 0, dbg_ridle = 0, dbg_rpark = 0, dbg_rend = 0, dbg_rstep = 0, dbg_rblock = 0;
 #endif
     // packet state (slot line 0) and trace state
     int slot = -1, mode = 0, pcell = 0, pface = 0, ncross = 0;
@@ -1035,9 +1042,26 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         // ends or parks sits out the rest of the iteration ("Several steps per
         // iteration").  (A compile-time count: a runtime one, a scalar compare per copy, cost
         // ray3d 3 %.)
+        // Trace-relative kernels: NREP steps in the radial form (a sphere beyond 1e-9 m: ~99.9 % of
+        // the crossings on the bench grid, 99.6 % on the cloudy one), then one generic step for
+        // every family and the reference's two-pass choice.  A lane whose next crossing is a
+        // theta / phi face, or lies within 1e-9 m, waits for that last step of the iteration: the
+        // radial form is then a straight sequence of instructions with no per-lane choice of the
+        // crossed family's index, no phi wrap and no index selects, and no join of two step forms
+        // (whose register copies cost more than the selects they saved).
+        constexpr int NSLOT = TREL ? NREP + 1 : NREP;
 #pragma unroll
-        for (int rep = 0; rep < NREP; rep++) {
+        for (int rep = 0; rep < NSLOT; rep++) {
+        const bool generic_slot = !TREL || rep == NREP;   // (a constant in every unrolled copy)
         TM_TICK(t_rep);   // (timing build: the evaluation is timed from each step's start)
+#ifdef ARTES_DEBUG_LANES
+        {   // per step: lanes idle, parked, ended in an earlier step of the iteration
+            dbg_rsteps++;
+            dbg_ridle += __popcll(__ballot(!have));
+            dbg_rpark += __popcll(__ballot(have && parked));
+            dbg_rend += __popcll(__ballot(have && !parked && end));
+        }
+#endif
         if (have && !parked && !end) {
             const double k = kext;
             // the nearest entry (TREL: a trace parameter) and its family; its distance from the
@@ -1208,177 +1232,224 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             // From the nearest entry best_abs of family w: the reference's two-pass choice when
             // that is not beyond 1e-9 m (ARTES.f90:3358-3418), next_cell (2671-2798), the
             // optical-depth sum and the trace ends (625-778, 848-941, 4739-4761)
+#ifdef ARTES_DEBUG_LANES
+            dbg_rstep += __popcll(__ballot(do_step));
+            dbg_rblock += __popcll(__ballot(!do_step));
+#endif
             if (do_step) {
-                if (!fast) {   // rare (every family exact here)
-                    const double r0 = TREL ? e0 - tpar : e0, r1 = TREL ? e1 - tpar : e1, r2 = TREL ? e2 - tpar : e2;
-                    const double t0 = or_nan(r0 > 1.e-9, r0);
-                    best = t0;
-                    w = 0;
-                    if constexpr (G3D) {
-                        const double t1 = or_nan(r1 > 1.e-9, r1), t2 = or_nan(r2 > 1.e-9, r2);
-                        best = min_nonan(min_nonan(t0, t1), t2);
-                        w = t0 == best ? 0 : (t1 == best ? 1 : 2);
-                    }
-                    if (!(best < INF)) {   // nothing beyond 1e-9 m
-                        best = r0 > 1.e-12 ? r0 : INF;
-                        w = 0;
-                        if constexpr (G3D) {
-                            if (r1 > 1.e-12 && r1 < best) { best = r1; w = 1; }
-                            if (r2 > 1.e-12 && r2 < best) { best = r2; w = 2; }
-                        }
-                    }
-                    best_abs = w == 0 ? e0 : (w == 1 ? e1 : e2);
-                }
-                // next_cell (ARTES.f90:2671-2798): the crossed family's index moves by one
-                // (phi wraps); the face index is the old one (inner face) or the new one
-                // (outer face) for every family
-                const bool side = (sides >> w) & 1;
-                const int kf = !G3D ? tcr : (w == 0 ? tcr : (w == 1 ? tct : tcp));
-                int kn = kf + (side ? 1 : -1);
-                if constexpr (G3D) {   // (branch-free: a divergent branch costs more scalar work)
-                    const int wrapped = kn < 0 ? G.nphi - 1 : (kn == G.nphi ? 0 : kn);
-                    kn = w == 2 ? wrapped : kn;
-                }
-                const int nfi = side ? kn : kf;
-                // a trace of 2^22 steps is a schedule or geometry bug, not a history (~100
-                // crossings per packet, a few thousand at most): drop the packet with error
-                // ARTES_ERR_RUNAWAY instead of spinning
-                const bool runaway = ncross >= nlim;
-                const bool err31 = !(best < K.inf) | runaway;
-                const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
-                const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
-                bool err = err31 | ((tft == 1) & (tfi == G.cell_depth) & surf);
+                if (!generic_slot) {
+                    if (w == 0 && fast) {
+                    // The radial form of the step (trace-relative kernels, see NSLOT): the generic
+                    // step below with w = 0 and a fast choice, the same results
+                    const int kn = tcr + ((sides & 1) ? 1 : -1);
+                    const bool side = sides & 1;
+                    const int nfi = side ? kn : tcr;
+                    const bool runaway = ncross >= nlim;
+                    const bool exit = side & (nfi == G.nr) & !runaway;
+                    const bool surf = (nfi == G.cell_depth) & !runaway;
+                    bool err = runaway | ((tft == 1) & (tfi == G.cell_depth) & surf);
     #ifdef ARTES_DEBUG
-                {   // the new index of the crossed family must name a cell unless the trace leaves
-                    // the grid or reaches the surface (ARTES_ERR_CELL: the packet is dropped before
-                    // its out-of-range kappa read, and the run fails)
-                    const int nk = !G3D ? G.nr : (w == 0 ? G.nr : (w == 1 ? G.ntheta : G.nphi));
-                    if (!err && !exit && !surf && (kn < 0 || kn >= nk)) {
+                    if (!err && !exit && !surf && (kn < 0 || kn >= G.nr)) {   // (ARTES_ERR_CELL, as below)
                         log_err(R, ARTES_ERR_CELL);
                         err = true;
                     }
-                }
     #endif
-                // (the error codes are logged on the chain-end paths below: every error stops)
-                auto log_step_err = [&]() {
-                    if (runaway) log_err(R, ARTES_ERR_RUNAWAY);
-                    log_err(R, err31 ? 31 : 34);
-                };
-                ncross++;
-                const double tau_cell = best * k;
-                const bool prop = (mode == S_PROP);
-                const bool hit = prop && tacc + tau_cell > ttgt;
-                const bool stop = err || exit || surf || hit;
+                    ncross++;
+                    const double tau_cell = best * k;
+                    const bool prop = (mode == S_PROP);
+                    const bool hit = prop && tacc + tau_cell > ttgt;
+                    const bool stop = err || exit || surf || hit;
     #ifdef ARTES_DEBUG_LANES
-                dbg_s = stop; dbg_h = prop && hit && !err; dbg_m = !stop; dbg_u = false;
+                    dbg_s = stop; dbg_h = prop && hit && !err; dbg_m = !stop; dbg_u = false;
     #endif
-                if constexpr (FLOW) {
-                    if (prop && !err && !hit) {   // the segment to the face (ARTES.f90:728-743, 889-904)
-                        const int lat = w == 0 ? (side ? 0 : 1) : (w == 1 ? (side ? 2 : 3) : -1);
-                        flow_segment(R.flow_g, R.flow_t, cell, tx + best * nx, ty + best * ny, tz + best * nz, nx, ny, nz, best, wI, lat);
-                    }
-                }
-                if constexpr (TREL) {
-                    // Every lane that crosses -- a move, or a trace end other than an interaction --
-                    // takes the crossing's optical depth, trace parameter and face; a move also
-                    // takes the new cell.  The trace ends are resolved once per iteration, after the
-                    // steps (below): inside every step their branches ran in ~90 % of the steps for
-                    // ~4 lanes (a lane that stops sits out the iteration's other steps either way).
                     const bool hitpark = prop & hit & !err;
                     if (!hitpark) {
                         tacc += tau_cell;
                         tpar = best_abs;
-                        tft = w + 1; tfi = nfi;
+                        tft = 1; tfi = nfi;
                     }
                     if (!stop) {
-                        if constexpr (G3D) {
-                            tcr = w == 0 ? kn : tcr;
-                            tct = w == 1 ? kn : tct;
-                            tcp = w == 2 ? kn : tcp;
-                            cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
-                        } else {
-                            cell += kn - kf;
-                            tcr = kn;
-                        }
+                        cell += kn - tcr;
+                        tcr = kn;
                         load_cell();
-                        pending |= 1 << w;
+                        pending |= 1;
                     } else {
-                        // the interaction waits, parked, until enough lanes of the wave need it (the
-                        // top of the loop); any other end waits for the end of the iteration
-                        parked = hitpark ? 4
-                                         : (PK_END | (exit ? PK_EXIT : 0) | (surf ? PK_SURF : 0) | (err31 ? PK_ERR31 : 0) |
-                                            (runaway ? PK_RUNAWAY : 0) | (err ? PK_ERR : 0));
+                        parked = hitpark ? 4 : (PK_END | (exit ? PK_EXIT : 0) | (surf ? PK_SURF : 0) | (runaway ? PK_ERR31 | PK_RUNAWAY : 0) |
+                                                (err ? PK_ERR : 0));
                     }
+                    }   // w == 0 && fast
                 } else {
-                    if (!stop) {
-                        tacc += tau_cell;
-                        if constexpr (TREL) {
-                            tpar = best_abs;
-                        } else {
-                            tx = fma(best, nx, tx); ty = fma(best, ny, ty); tz = fma(best, nz, tz);
-                        }
-                        tft = w + 1; tfi = nfi;
+                    if (!fast) {   // rare (every family exact here)
+                        const double r0 = TREL ? e0 - tpar : e0, r1 = TREL ? e1 - tpar : e1, r2 = TREL ? e2 - tpar : e2;
+                        const double t0 = or_nan(r0 > 1.e-9, r0);
+                        best = t0;
+                        w = 0;
                         if constexpr (G3D) {
-                            tcr = w == 0 ? kn : tcr;
-                            tct = w == 1 ? kn : tct;
-                            tcp = w == 2 ? kn : tcp;
-                            cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
-                            if constexpr (!TREL) { e0 -= best; e1 -= best; e2 -= best; }
-                        } else {
-                            cell += kn - kf;
-                            tcr = kn;
+                            const double t1 = or_nan(r1 > 1.e-9, r1), t2 = or_nan(r2 > 1.e-9, r2);
+                            best = min_nonan(min_nonan(t0, t1), t2);
+                            w = t0 == best ? 0 : (t1 == best ? 1 : 2);
                         }
-                        load_cell();
-                        pending |= 1 << w;
-                    } else if (prop && !err && hit) {
-                        // the interaction in this cell waits, parked, until enough lanes of the
-                        // wave need it (the top of the loop)
-                        parked = 4;
-                    } else if (prop) {
-                        if (err) {
-                            log_step_err();
-                            log_err(R, 3);
-                            end = S_END_DROP;
-                        } else if (exit) {                             // left the atmosphere
-                            end = S_END_EXIT;
-                        } else {                                       // reached the surface (ARTES.f90:755-774)
-                            // (xi > albedo: absorbed; a black surface absorbs whatever xi is, and
-                            // an ended packet's RNG state is not used again, so no draw then)
-                            bool absorbed = true;
-                            if (R.surface_albedo > 0.0) absorbed = rng.uni() > R.surface_albedo;
-                            if (absorbed) {
-                                end = S_END_ABS;
-                            } else {
-                                // Lambertian reflection: k_event turns the packet at the surface point,
-                                // the propagation then resumes with the optical depth still to go
-                                const double sf = TREL ? best_abs : best;
-                                px = tx + sf * nx; py = ty + sf * ny; pz = tz + sf * nz;
-                                pcell = pack_cell(tcr, tct, tcp);
-                                pface = pack_face(1, G.cell_depth);
-                                ttgt = ttgt - (tacc + tau_cell);
-                                end = S_SURF_HIT;
+                        if (!(best < INF)) {   // nothing beyond 1e-9 m
+                            best = r0 > 1.e-12 ? r0 : INF;
+                            w = 0;
+                            if constexpr (G3D) {
+                                if (r1 > 1.e-12 && r1 < best) { best = r1; w = 1; }
+                                if (r2 > 1.e-12 && r2 < best) { best = r2; w = 2; }
                             }
                         }
-                    } else {   // a first-optical-depth or peel-off trace reached the boundary
-                        tacc += tau_cell;
-                        // error codes of the four traces (ARTES.f90:640, 4743, 4549, 4653)
-                        if (err) {
-                            log_step_err();
-                            log_err(R, mode == S_FIRST ? 2 : mode == S_PEEL ? 43 : mode == S_PEEL_T ? 46 : 42);
+                        best_abs = w == 0 ? e0 : (w == 1 ? e1 : e2);
+                    }
+                    // next_cell (ARTES.f90:2671-2798): the crossed family's index moves by one
+                    // (phi wraps); the face index is the old one (inner face) or the new one
+                    // (outer face) for every family
+                    const bool side = (sides >> w) & 1;
+                    const int kf = !G3D ? tcr : (w == 0 ? tcr : (w == 1 ? tct : tcp));
+                    int kn = kf + (side ? 1 : -1);
+                    if constexpr (G3D) {   // (branch-free: a divergent branch costs more scalar work)
+                        const int wrapped = kn < 0 ? G.nphi - 1 : (kn == G.nphi ? 0 : kn);
+                        kn = w == 2 ? wrapped : kn;
+                    }
+                    const int nfi = side ? kn : kf;
+                    // a trace of 2^22 steps is a schedule or geometry bug, not a history (~100
+                    // crossings per packet, a few thousand at most): drop the packet with error
+                    // ARTES_ERR_RUNAWAY instead of spinning
+                    const bool runaway = ncross >= nlim;
+                    const bool err31 = !(best < K.inf) | runaway;
+                    const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
+                    const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
+                    bool err = err31 | ((tft == 1) & (tfi == G.cell_depth) & surf);
+        #ifdef ARTES_DEBUG
+                    {   // the new index of the crossed family must name a cell unless the trace leaves
+                        // the grid or reaches the surface (ARTES_ERR_CELL: the packet is dropped before
+                        // its out-of-range kappa read, and the run fails)
+                        const int nk = !G3D ? G.nr : (w == 0 ? G.nr : (w == 1 ? G.ntheta : G.nphi));
+                        if (!err && !exit && !surf && (kn < 0 || kn >= nk)) {
+                            log_err(R, ARTES_ERR_CELL);
+                            err = true;
                         }
-                        if (is_peel_trace(mode)) {
-                            const int kind = mode == S_PEEL_T ? 1 : mode == S_PEEL_S ? 2 : 0;
-                            end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0) | (kind << PEEL_KIND_SHIFT);
-                        } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
-                            end = S_END_DROP;
-                        } else {
-                            // the forced first interaction waits (parked, at the chord's far end:
-                            // the position, face and cell of the crossing, for a backward walk)
-                            // until enough lanes of the wave need it (see the top of the loop)
-                            const double sf = TREL ? best_abs : best;
-                            tx += sf * nx; ty += sf * ny; tz += sf * nz;
+                    }
+        #endif
+                    // (the error codes are logged on the chain-end paths below: every error stops)
+                    auto log_step_err = [&]() {
+                        if (runaway) log_err(R, ARTES_ERR_RUNAWAY);
+                        log_err(R, err31 ? 31 : 34);
+                    };
+                    ncross++;
+                    const double tau_cell = best * k;
+                    const bool prop = (mode == S_PROP);
+                    const bool hit = prop && tacc + tau_cell > ttgt;
+                    const bool stop = err || exit || surf || hit;
+        #ifdef ARTES_DEBUG_LANES
+                    dbg_s = stop; dbg_h = prop && hit && !err; dbg_m = !stop; dbg_u = false;
+        #endif
+                    if constexpr (FLOW) {
+                        if (prop && !err && !hit) {   // the segment to the face (ARTES.f90:728-743, 889-904)
+                            const int lat = w == 0 ? (side ? 0 : 1) : (w == 1 ? (side ? 2 : 3) : -1);
+                            flow_segment(R.flow_g, R.flow_t, cell, tx + best * nx, ty + best * ny, tz + best * nz, nx, ny, nz, best, wI, lat);
+                        }
+                    }
+                    if constexpr (TREL) {
+                        // Every lane that crosses -- a move, or a trace end other than an interaction --
+                        // takes the crossing's optical depth, trace parameter and face; a move also
+                        // takes the new cell.  The trace ends are resolved once per iteration, after the
+                        // steps (below): inside every step their branches ran in ~90 % of the steps for
+                        // ~4 lanes (a lane that stops sits out the iteration's other steps either way).
+                        const bool hitpark = prop & hit & !err;
+                        if (!hitpark) {
+                            tacc += tau_cell;
+                            tpar = best_abs;
                             tft = w + 1; tfi = nfi;
-                            parked = err ? 3 : 1;
+                        }
+                        if (!stop) {
+                            if constexpr (G3D) {
+                                tcr = w == 0 ? kn : tcr;
+                                tct = w == 1 ? kn : tct;
+                                tcp = w == 2 ? kn : tcp;
+                                cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
+                            } else {
+                                cell += kn - kf;
+                                tcr = kn;
+                            }
+                            load_cell();
+                            pending |= 1 << w;
+                        } else {
+                            // the interaction waits, parked, until enough lanes of the wave need it (the
+                            // top of the loop); any other end waits for the end of the iteration
+                            parked = hitpark ? 4
+                                             : (PK_END | (exit ? PK_EXIT : 0) | (surf ? PK_SURF : 0) | (err31 ? PK_ERR31 : 0) |
+                                                (runaway ? PK_RUNAWAY : 0) | (err ? PK_ERR : 0));
+                        }
+                    } else {
+                        if (!stop) {
+                            tacc += tau_cell;
+                            if constexpr (TREL) {
+                                tpar = best_abs;
+                            } else {
+                                tx = fma(best, nx, tx); ty = fma(best, ny, ty); tz = fma(best, nz, tz);
+                            }
+                            tft = w + 1; tfi = nfi;
+                            if constexpr (G3D) {
+                                tcr = w == 0 ? kn : tcr;
+                                tct = w == 1 ? kn : tct;
+                                tcp = w == 2 ? kn : tcp;
+                                cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
+                                if constexpr (!TREL) { e0 -= best; e1 -= best; e2 -= best; }
+                            } else {
+                                cell += kn - kf;
+                                tcr = kn;
+                            }
+                            load_cell();
+                            pending |= 1 << w;
+                        } else if (prop && !err && hit) {
+                            // the interaction in this cell waits, parked, until enough lanes of the
+                            // wave need it (the top of the loop)
+                            parked = 4;
+                        } else if (prop) {
+                            if (err) {
+                                log_step_err();
+                                log_err(R, 3);
+                                end = S_END_DROP;
+                            } else if (exit) {                             // left the atmosphere
+                                end = S_END_EXIT;
+                            } else {                                       // reached the surface (ARTES.f90:755-774)
+                                // (xi > albedo: absorbed; a black surface absorbs whatever xi is, and
+                                // an ended packet's RNG state is not used again, so no draw then)
+                                bool absorbed = true;
+                                if (R.surface_albedo > 0.0) absorbed = rng.uni() > R.surface_albedo;
+                                if (absorbed) {
+                                    end = S_END_ABS;
+                                } else {
+                                    // Lambertian reflection: k_event turns the packet at the surface point,
+                                    // the propagation then resumes with the optical depth still to go
+                                    const double sf = TREL ? best_abs : best;
+                                    px = tx + sf * nx; py = ty + sf * ny; pz = tz + sf * nz;
+                                    pcell = pack_cell(tcr, tct, tcp);
+                                    pface = pack_face(1, G.cell_depth);
+                                    ttgt = ttgt - (tacc + tau_cell);
+                                    end = S_SURF_HIT;
+                                }
+                            }
+                        } else {   // a first-optical-depth or peel-off trace reached the boundary
+                            tacc += tau_cell;
+                            // error codes of the four traces (ARTES.f90:640, 4743, 4549, 4653)
+                            if (err) {
+                                log_step_err();
+                                log_err(R, mode == S_FIRST ? 2 : mode == S_PEEL ? 43 : mode == S_PEEL_T ? 46 : 42);
+                            }
+                            if (is_peel_trace(mode)) {
+                                const int kind = mode == S_PEEL_T ? 1 : mode == S_PEEL_S ? 2 : 0;
+                                end = S_PEEL_DONE | (exit ? FLAG_EXIT : 0) | (err ? FLAG_ERR : 0) | (kind << PEEL_KIND_SHIFT);
+                            } else if (tacc < 1.e-6 && !surf) {            // forced first interaction (ARTES.f90:658-685)
+                                end = S_END_DROP;
+                            } else {
+                                // the forced first interaction waits (parked, at the chord's far end:
+                                // the position, face and cell of the crossing, for a backward walk)
+                                // until enough lanes of the wave need it (see the top of the loop)
+                                const double sf = TREL ? best_abs : best;
+                                tx += sf * nx; ty += sf * ny; tz += sf * nz;
+                                tft = w + 1; tfi = nfi;
+                                parked = err ? 3 : 1;
+                            }
                         }
                     }
                 }
@@ -1505,6 +1576,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         atomicAdd(&R.err[22], dbg_anyf12);
         atomicAdd(&R.err[23], dbg_f2);
         atomicAdd(&R.err[24], dbg_anyf2);
+        atomicAdd(&R.err[49], dbg_rsteps);
+        atomicAdd(&R.err[50], dbg_ridle);
+        atomicAdd(&R.err[51], dbg_rpark);
+        atomicAdd(&R.err[52], dbg_rend);
+        atomicAdd(&R.err[53], dbg_rstep);
+        atomicAdd(&R.err[54], dbg_rblock);
     }
 #endif
     const unsigned long long wv = wave_sum_u64(c_cross), wp = wave_sum_u64(c_peel);

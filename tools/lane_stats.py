@@ -26,6 +26,9 @@ for name in (os.environ.get("LS_WORKLOAD", "ray3d"),):
     det = driver.detector_geometry(cfg, atm["radial"][-1])
     g = Grid(atm, 0)
     g.set_profiling(True)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import _tuning
+    _tuning.apply(g)
     p = driver.run_params(cfg, det, 0, det_phi=1e-5 if name == "cloudy" else None, cell_depth=g.cell_depth(0),
                           packet_moments=False)
     for env in variants:
@@ -55,6 +58,10 @@ for name in (os.environ.get("LS_WORKLOAD", "ray3d"),):
               f"theta / phi evaluations {f12 / steps:.2f} lanes per wave-step, in {anyf12 / steps:.3f} of iterations "
               f"(phi: {f2 / steps:.2f} lanes, in {anyf2 / steps:.3f})",
               flush=True)
+        rs = max(int(r.err[49]), 1)
+        print(f"  per step of an iteration (of 64 lanes): idle {r.err[50] / rs:.2f}, parked {r.err[51] / rs:.2f}, "
+              f"ended earlier in the iteration {r.err[52] / rs:.2f}, stepping {r.err[53] / rs:.2f}, "
+              f"evaluating without a step {r.err[54] / rs:.2f}; crossings per step {C / rs:.2f}", flush=True)
         for k, v in old.items():
             if v is None:
                 os.environ.pop(k, None)

@@ -26,6 +26,9 @@ else:
     atm = synthetic.make_config(name, share_matrix=True)
 det = driver.detector_geometry(cfg, atm["radial"][-1])
 g = Grid(atm, 0)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _tuning
+_tuning.apply(g)
 g.set_profiling(True)
 p = driver.run_params(cfg, det, 0, det_phi=1e-5 if name == "cloudy" else None, cell_depth=g.cell_depth(0),
                       packet_moments=False)
