@@ -207,6 +207,9 @@ constexpr double INF = __builtin_inf();
 // interaction waits; PK_END and its bits (trace-relative kernels): a trace end found in a step,
 // resolved at the end of the iteration
 enum : int { PK_END = 8, PK_EXIT = 16, PK_SURF = 32, PK_ERR31 = 64, PK_RUNAWAY = 128, PK_ERR = 256 };
+// a new trace's set-up (k_trace's common set-up block): the start cell from the packet position,
+// the direction's constants
+enum : int { NT_POS = 1, NT_DIR = 2 };
 
 // x if valid, else a NaN: only the high word is selected (one v_cndmask instead of two
 // for a double select).  min_nonan ignores the NaN, and every compare with it is false, so
@@ -643,6 +646,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     int nlim = 0;   // the packet's crossing count at which the current trace is a runaway
     int parked = 0;   // 1: waiting for the batched forced first interaction (3: after a cell error)
     int pend = 0;     // the end mode of a chain whose list append waits for the wave's next refill
+    int nt = 0;       // a new trace waits for the iteration's common set-up: NT_POS (the start cell) | NT_DIR
+    // (3D grids; the radial-only kernel sets its cheap traces up where they start: the flag would
+    // take it past 102 registers, its 5th wave per SIMD)
+    constexpr bool SETUP_MERGED = G3D;
 
     // Lazy set-up (3D grids, one-face evaluation).  A new trace needs every family's
     // distance before its first step, one family per iteration, so two of every trace's
@@ -728,28 +735,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         if constexpr (G3D && !TREL) inz = fast_rcp(nz);
         set_trel();
     };
-    // every peel-off trace runs along the detector direction: its constants once (3D
-    // grids; radial-only grids recompute them, registers for a 5th wave)
-    double det_Axy = 0.0, det_Az = 0.0, det_inz = 0.0;
-    if constexpr (G3D && !TREL) {
-        det_Axy = dir_axy(ax2, by2, R.det0, R.det1);
-        det_Az = cz2 * R.det2 * R.det2;
-        det_inz = fast_rcp(R.det2);
-    }
-    auto set_direction_det = [&]() {
-        if constexpr (G3D) {
-            nx = R.det0; ny = R.det1; nz = R.det2;
-            if constexpr (!TREL) { Axy = det_Axy; Az = det_Az; inz = det_inz; }
-            tacc = 0.0;
-            nlim = ncross + (1 << 22);
-            pending = fam_all;
-            sides = 0;
-            set_bounds();
-            set_trel();
-        } else {
-            set_direction(R.det0, R.det1, R.det2);
-        }
-    };
     // a trace starts at the packet position with zero optical depth
     auto start_position = [&]() {
         tx = px; ty = py; tz = pz;
@@ -763,10 +748,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 #endif
         cell = tcr + (int)__umul24((unsigned)G.nr, (unsigned)tct) + (int)__umul24((unsigned)nrt, (unsigned)tcp);
         load_cell();
-    };
-    auto start_trace = [&](double d0, double d1, double d2) {
-        start_position();
-        set_direction(d0, d1, d2);
     };
 
     // The forced first interaction at the end of a first trace (ARTES.f90:658-685): one
@@ -794,14 +775,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         kb = back ? 2 * ncross + (ncross - kb) + 1 : 0;
         // (one set_direction for both walks, on selected operands: the two inlined copies ran
         // as a divergent pair, ~65 VALU instructions more per block)
-        if (back) {
-            ttgt = fmax(tau_first - tau, 0.0);   // tau rounds to <= tau_first + 1 ulp
+        // (3D grids: the new trace's set-up waits for the iteration's common set-up block, below)
+        ttgt = back ? fmax(tau_first - tau, 0.0) : tau;   // (tau rounds to <= tau_first + 1 ulp)
+        if (back) { nx = -nx; ny = -ny; nz = -nz; }
+        if constexpr (SETUP_MERGED) {
+            nt = back ? NT_DIR : NT_POS | NT_DIR;
         } else {
-            ttgt = tau;
-            start_position();
+            if (!back) start_position();
+            set_direction(nx, ny, nz);
         }
-        const double sgn = back ? -1.0 : 1.0;
-        set_direction(sgn * nx, sgn * ny, sgn * nz);
     };
 
     // The interaction at the end of a propagation (ARTES.f90:705-720), then the
@@ -847,7 +829,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         mode = S_PEEL;
         tx = px; ty = py; tz = pz;
         tft = 0; tfi = 0;
-        set_direction_det();
+        nx = R.det0; ny = R.det1; nz = R.det2;
+        if constexpr (SETUP_MERGED) nt = NT_DIR;   // (the set-up: the iteration's common block, below)
+        else set_direction(nx, ny, nz);
         return 0;
     };
 
@@ -998,7 +982,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     did = true;
 #endif
                     const bool peel = is_peel_trace(mode);
-                    start_trace(peel ? R.det0 : ldx, peel ? R.det1 : ldy, peel ? R.det2 : ldz);
+                    nx = peel ? R.det0 : ldx; ny = peel ? R.det1 : ldy; nz = peel ? R.det2 : ldz;
+                    if constexpr (SETUP_MERGED) {
+                        nt = NT_POS | NT_DIR;   // (the set-up: the common block below)
+                    } else {
+                        start_position();
+                        set_direction(nx, ny, nz);
+                    }
                     have = true;
                     kb = (mode == S_FIRST) ? ncross : 0;
                 }
@@ -1018,6 +1008,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 }
 #endif
             }
+        }
+        // The new traces of this iteration -- the forced first interactions' propagations, the
+        // interactions' peel-offs and the refilled slots' traces -- set up together: the start
+        // cell (unless a backward walk starts where the first trace stopped), the direction's
+        // constants, the lazy bounds and the trace-relative constants run once per iteration for
+        // all of them, instead of once in each of the three blocks
+        if (SETUP_MERGED && __ballot(nt != 0)) {
+            TM_TICK(ts0);
+            if (nt & NT_POS) start_position();
+            if (nt) set_direction(nx, ny, nz);
+            nt = 0;
+            TM_TICK(ts1);
+            TM_ADD(12, ts1 - ts0);
         }
         TM_TICK(t2);
         TM_ADD(1, t2 - t1);

@@ -17,7 +17,15 @@ def env_tuning(env=None) -> dict:
 
 
 def apply(grid, env=None) -> dict:
-    kv = env_tuning(env)
-    if kv:
-        grid.set_tuning(**kv)
-    return kv
+    """Set what the handle accepts; a key it rejects (e.g. steps=4 on a radial-only grid) is
+    reported and left at its default."""
+    from artes_amd.engine import EngineError
+
+    kv, done = env_tuning(env), {}
+    for k, v in kv.items():
+        try:
+            grid.set_tuning(**{k: v})
+            done[k] = v
+        except EngineError as e:
+            print(f"[tuning] {k}={v} not applied: {e}", flush=True)
+    return done
