@@ -396,6 +396,51 @@ __device__ __forceinline__ void polarization_rotation(const DevRun& R, double al
                              peeling);
 }
 
+// The peel-off's polarization rotation (ARTES.f90:4864-4920): the Stokes vector st scattered
+// by the interpolated matrix sc towards the detector (mu = cos of the scattering angle), in
+// so[]; false when the reference skips the contribution (error 45) or drops the packet
+// (error 49, `drop`).  (cpo, spo) is the incoming direction's azimuth (azimuth_cs).
+// The rotation angle phs = acos(num), or its clamps 1e-10 / pi - 1e-10 (0 for a NaN), turned
+// to 2 pi - phs when (phi_old - phi_det) mod 2 pi lies in [0, pi), enters polarization_rotation
+// only through mueller(phs) and its half-turn: cos(2 phs) = 2 x^2 - 1 (x = num, or +-1 at
+// the clamps, where the reference's cos(2 phs) rounds to 1), the sine negative on phs in
+// (pi/2, pi) (x < 0) and on (3 pi/2, 2 pi) (turned, x > 0); no acos and no cosine.  The
+// turn is decided from the azimuths' cosines and sines: sin(phi_old - phi_det) > 0, or the
+// azimuths equal.  Where the difference is within rounding of 0 or pi the two forms can
+// decide the turn differently.  There the direction, the detector and z lie in one plane,
+// num = +-1 and sin(2 phs) ~ 0, so either turn gives the same vector -- unless the direction
+// is within ~1e-6 rad of vertical, where num (through sqrt(1 - dz^2)) carries a relative
+// error up to ~1e-4 in both forms and the turn is a rounding decision in the reference too
+// (tests/test_gpu_unit_checks.py accepts either turn there, and checks every other case to
+// 1e-7).
+__device__ __forceinline__ bool peel_rotation(const DevRun& R, double dz, double mu, double cpo, double spo,
+                                              const double st[4], const double sc[16], double so[4], bool& drop) {
+    if (!(fabs(dz) < 1.0)) {
+        log_err(R, 45);
+        return false;
+    }
+    const double num = (R.det2 - dz * mu) / (dsqrt(1.0 - mu * mu) * dsqrt(1.0 - dz * dz));
+    double x = 1.0;
+    bool nan = false;
+    if (fabs(num) < 1.0) x = num;
+    else if (num >= 1.0) x = 1.0;
+    else if (num <= -1.0) x = -1.0;
+    else { log_err(R, 44); nan = true; }
+    // (phi_old - phi_det) mod 2 pi in [0, pi): its sine > 0, or the azimuths equal
+    const double sd = spo * R.cdphi - cpo * R.sdphi, cd = cpo * R.cdphi + spo * R.sdphi;
+    const bool flip = sd > 0.0 || (sd == 0.0 && cd > 0.0);
+    const double c2p = fma(2.0 * x, x, -1.0);
+    double s2p = dsqrt(1.0 - c2p * c2p);
+    if (flip ? (x > 0.0 && !nan) : (x < 0.0)) s2p = -s2p;
+    if (!(fabs(mu) < 1.0)) {
+        log_err(R, 49);
+        drop = true;
+        return false;
+    }
+    polarization_rotation_cs(R, mu, c2p, s2p, !flip, flip && !nan, st, sc, dz, R.det2, so, true);
+    return true;
+}
+
 // the azimuth of direction (d0, d1) in [0, 2 pi) as direction_cosine takes it (ARTES.f90:1975-1977)
 __device__ __forceinline__ double azimuth(double d0, double d1) {
     double phi = atan2(d1, d0);

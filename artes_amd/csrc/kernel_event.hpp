@@ -624,38 +624,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             else if (mu <= -1.0) mu = -1.0 + 1.e-10;
             double sc[16];
             interp_matrix<TL::RS, TL::RS4>(P, sym, acos(mu), sc);
-            bool have_out = false;
             double so[4] = {0, 0, 0, 0};
-            if (fabs(dz) < 1.0) {
-                // the rotation angle phs (4872-4916) = acos(num), or its clamps 1e-10 / pi - 1e-10
-                // (0 for a NaN), turned to 2 pi - phs when (phi_old - phi_det) mod 2 pi lies in
-                // [0, pi).  It enters polarization_rotation only through mueller(phs) and its
-                // half-turn: cos(2 phs) = 2 x^2 - 1 (x = num, or +-1 at the clamps, where the
-                // reference's cos(2 phs) rounds to 1), the sine negative on phs in (pi/2, pi)
-                // (x < 0) and on (3 pi/2, 2 pi) (turned, x > 0); no acos and no cosine
-                const double num = (R.det2 - dz * mu) / (dsqrt(1.0 - mu * mu) * dsqrt(1.0 - dz * dz));
-                double x = 1.0;
-                bool nan = false;
-                if (fabs(num) < 1.0) x = num;
-                else if (num >= 1.0) x = 1.0;
-                else if (num <= -1.0) x = -1.0;
-                else { log_err(R, 44); nan = true; }
-                // (phi_old - phi_det) mod 2 pi in [0, pi): its sine > 0, or the azimuths equal
-                const double sd = spo * R.cdphi - cpo * R.sdphi, cd = cpo * R.cdphi + spo * R.sdphi;
-                const bool flip = sd > 0.0 || (sd == 0.0 && cd > 0.0);
-                const double c2p = fma(2.0 * x, x, -1.0);
-                double s2p = dsqrt(1.0 - c2p * c2p);
-                if (flip ? (x > 0.0 && !nan) : (x < 0.0)) s2p = -s2p;
-                if (fabs(mu) < 1.0) {
-                    polarization_rotation_cs(R, mu, c2p, s2p, !flip, flip && !nan, st, sc, dz, R.det2, so, true);
-                    have_out = true;
-                } else {
-                    log_err(R, 49);
-                    drop = true;
-                }
-            } else {
-                log_err(R, 45);
-            }
+            const bool have_out = peel_rotation(R, dz, mu, cpo, spo, st, sc, so, drop);
             if (have_out && !drop) {
                 const double x_im = py * R.cdp - px * R.sdp;
                 const double y_im = pz * R.sdt - py * R.cdt * R.sdp - px * R.cdt * R.cdp;
@@ -923,8 +893,8 @@ __device__ __forceinline__ void emit_planet(const DevGrid& G, const DevRun& R, R
 // to position out0 + i of the output trace list (see Lists), a hole (-1)
 // when the ids have run out: list positions and packet ids need no atomics, and the
 // packet-to-slot assignment is deterministic.  k_rotate advances next_pkt and the count.
-// doubles of LDS k_emit stages for initial_cell: theta faces [ntheta+1], phi faces [nphi] + 2 pi
-__host__ __device__ inline size_t emit_table_doubles(int ntheta, int nphi) { return (size_t)ntheta + 1 + nphi + 1; }
+// doubles of LDS k_emit stages for initial_cell: keys and faces of theta [ntheta+1] and phi [nphi] + 1
+__host__ __device__ inline size_t emit_table_doubles(int ntheta, int nphi) { return 2 * ((size_t)ntheta + 1 + nphi + 1); }
 
 // the cell j of ascending faces f[0..n] with f[j] < v < f[j+1], or 0 when v sits on a face
 // or outside: the cell initial_cell's linear scan finds (ARTES.f90:2630-2660).  Binary
@@ -939,16 +909,75 @@ __device__ __forceinline__ int face_interval(const double* f, int n, double v) {
     return (j >= 0 && v < f[j + 1]) ? j : 0;
 }
 
+// face_interval over an increasing key of the angle (k_emit's initial_cell): the same cell as
+// the search over the angle itself whenever the key lies 1e-9 or more from both bounding
+// faces' keys (the keys below grow no faster than their angle, so the angle is then 1e-9 rad
+// or more from the faces, far beyond the rounding of acos / atan2); `near` otherwise (or NaN)
+__device__ __forceinline__ int key_interval(const double* f, int n, double v, bool& near) {
+    int lo = 0, hi = n - 1, j = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (f[mid] < v) { j = mid; lo = mid + 1; }
+        else hi = mid - 1;
+    }
+    const int jj = j < 0 ? 0 : j;
+    near = !(v - f[jj] >= 1.e-9 && f[jj + 1] - v >= 1.e-9);
+    return jj;
+}
+
+// a key of the angle atan2(y, x) in [0, 2 pi) that grows with it, in [0, 4): one unit per
+// quadrant, a ratio of |x| or |y| to |x| + |y| (no atan2).  d key / d angle = 1 / (|cos| +
+// |sin|)^2, in [1/2, 1]
+__device__ __forceinline__ double phi_key(double x, double y) {
+    const double ax = fabs(x), ay = fabs(y), q = 1.0 / (ax + ay);
+    if (!(y < 0.0)) return x >= 0.0 ? ay * q : 1.0 + ax * q;
+    return x < 0.0 ? 2.0 + ay * q : 3.0 + ax * q;
+}
+
+// Store every lane's 128-byte line, staged in LDS at st[9 * lane ...], to `dst` (null:
+// none), the whole wave together (wave-uniform control flow): groups of 8 lanes write 16
+// bytes each, so every store instruction writes 8 whole lines.  Written per lane, each of
+// the 8 instructions would touch 64 lines, one 16-byte piece of each.
+constexpr int LINE_STAGE = 64 * 9;   // uint4 per wave: 64 lines of 8 pieces, padded to 9
+__device__ __forceinline__ void wave_store_lines(const uint4* st, void* dst) {
+    const int l = threadIdx.x & 63;
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long d = (unsigned long long)dst;
+    const int lo = (int)(unsigned)d, hi = (int)(d >> 32);
+    const int piece = l & 7;
+#pragma unroll 1
+    for (int r = 0; r < 8; r++) {
+        const int src = r * 8 + (l >> 3);
+        const unsigned long long a = ((unsigned long long)(unsigned)__shfl(hi, src) << 32) | (unsigned)__shfl(lo, src);
+        if (a) reinterpret_cast<uint4*>(a)[piece] = st[src * 9 + piece];
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <bool G3D, bool TRACE>
 __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, SubLists SL) {
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_em[];
-    double* s_tf = s_em;                      // theta faces
-    double* s_pf = s_em + (G.ntheta + 1);     // phi faces, then 2 pi
+    __shared__ uint4 s_lines[BLOCK / 64 * LINE_STAGE];
+    // initial_cell's searches, over keys of the angles: -cos(theta) of the theta faces, phi_key
+    // of the phi faces (then 4); the faces themselves for the rare position near a face
+    double* s_tk = s_em;                          // [ntheta + 1]
+    double* s_pk = s_tk + (G.ntheta + 1);         // [nphi + 1]
+    double* s_tf = s_pk + (G.nphi + 1);           // [ntheta + 1]
+    double* s_pf = s_tf + (G.ntheta + 1);         // [nphi + 1]: the faces, then 2 pi
     if constexpr (G3D) {
-        for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) s_tf[i] = G.thetaf[i];
-        for (int i = threadIdx.x; i < G.nphi; i += BLOCK) s_pf[i] = G.phif[i];
-        if (threadIdx.x == 0) s_pf[G.nphi] = TWO_PI;
+        for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) {
+            s_tk[i] = -G.tcos[i];
+            s_tf[i] = G.thetaf[i];
+        }
+        for (int i = threadIdx.x; i < G.nphi; i += BLOCK) {
+            s_pk[i] = phi_key(G.phic[i], G.phis[i]);
+            s_pf[i] = G.phif[i];
+        }
+        if (threadIdx.x == 0) {
+            s_pk[G.nphi] = 4.0;
+            s_pf[G.nphi] = TWO_PI;
+        }
         __syncthreads();
     }
     const int n = *L.emit_n;
@@ -999,6 +1028,8 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
         const unsigned long long k = pkt0 + (unsigned long long)i;
         const bool emit = slot >= 0 && k < L.n;
         if (slot >= 0 && !emit) S.s[slot].mode = S_RETIRED;
+        uint4* const st = s_lines + (threadIdx.x >> 6) * LINE_STAGE;
+        Line0& rec = *reinterpret_cast<Line0*>(st + (threadIdx.x & 63) * 9);   // (stored below by the whole wave)
         if (emit) {
         c_pkt++;
         const unsigned long long pid = L.first + k;
@@ -1043,24 +1074,30 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
             dx = sin_b(td) * cos_b(pd); dy = sin_b(td) * sin_b(pd); dz = cos_b(td);
         }
         if constexpr (G3D) {   // initial_cell (ARTES.f90:2605-2669)
+            // (the searches over keys of the angles; acos / atan2 only near a face, ~1e-7 of the
+            // packets: they were ~30 % of k_emit's instructions)
             const double r = sqrt(px * px + py * py + pz * pz);
-            const double th = acos(pz / r);
-            double ph = atan2(py, px);
-            if (ph < 0.0) ph += TWO_PI;
-            ct = face_interval(s_tf, G.ntheta, th);
-            cp = face_interval(s_pf, G.nphi, ph);
+            bool near_t, near_p;
+            ct = key_interval(s_tk, G.ntheta, -(pz / r), near_t);
+            cp = key_interval(s_pk, G.nphi, phi_key(px, py), near_p);
+            if (near_t) ct = face_interval(s_tf, G.ntheta, acos(pz / r));
+            if (near_p) {
+                double ph = atan2(py, px);
+                if (ph < 0.0) ph += TWO_PI;
+                cp = face_interval(s_pf, G.nphi, ph);
+            }
         }
         }   // star
-        S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
-        S.s[slot].px = px; S.s[slot].py = py; S.s[slot].pz = pz;
-        S.s[slot].dx = dx; S.s[slot].dy = dy; S.s[slot].dz = dz;
-        S.s[slot].q1 = 0.0; S.s[slot].q2 = 0.0; S.s[slot].q3 = 0.0;
-        S.s[slot].wI = wI;
-        S.s[slot].pcell = pack_cell(cr, ct, cp); S.s[slot].pface = face;
-        S.s[slot].ttgt = 0.0;
-        S.s[slot].tpeel = 0.0;
-        S.s[slot].ncross = 0;
-        S.s[slot].mode = mode0;
+        rec.r0 = rng.s0; rec.r1 = rng.s1;
+        rec.px = px; rec.py = py; rec.pz = pz;
+        rec.dx = dx; rec.dy = dy; rec.dz = dz;
+        rec.q1 = 0.0; rec.q2 = 0.0; rec.q3 = 0.0;
+        rec.wI = wI;
+        rec.pcell = pack_cell(cr, ct, cp); rec.pface = face;
+        rec.ttgt = 0.0;
+        rec.tpeel = 0.0;
+        rec.ncross = 0;
+        rec.mode = mode0;
         if (R.moments) {
             S.d[slot].cs0 = S.d[slot].cs1 = S.d[slot].cs2 = S.d[slot].cs3 = 0.0;
             S.d[slot].pt0 = S.d[slot].pt1 = S.d[slot].pt2 = S.d[slot].pt3 = 0.0;
@@ -1073,6 +1110,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
             S.d[slot].nscat = 0;
         }
         }   // emit
+        wave_store_lines(st, emit ? (void*)&S.s[slot] : nullptr);
 #ifdef ARTES_DEBUG
         if (i < n && out0 + i >= L.P) atomicAdd(&R.err[ARTES_ERR_LISTS], 1ULL);   // (L2: no write past the list)
         if (i < n && out0 + i < L.P) L.trace_out[out0 + i] = emit ? slot : -1;

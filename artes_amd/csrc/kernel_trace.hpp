@@ -1036,12 +1036,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         // The evaluation and the step, NREP times per iteration (unrolled): the iteration's
         // wave-level blocks -- parked-lane ballots and blocks, refill check and refill,
         // chain-end stores, queue flushes, loop head -- run once per NREP steps.  A lane that
-        // ends, parks or waits for a theta batch sits out the rest of the iteration (DESIGN.md
-        // §4, "Several steps per iteration").  (A compile-time count: a runtime one, a scalar
-        // compare per copy, cost ray3d 3 %.)
-        // The evaluation and the step, NREP times per iteration (unrolled): the iteration's
-        // wave-level blocks -- parked-lane ballots and blocks, refill check and refill,
-        // chain-end stores, queue flushes, loop head -- run once per NREP steps.  A lane that
         // ends or parks sits out the rest of the iteration ("Several steps per
         // iteration").  (A compile-time count: a runtime one, a scalar compare per copy, cost
         // ray3d 3 %.)
@@ -1116,7 +1110,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     const int fam = fast ? w : __builtin_ctz(pending & 6);
                     // (both ballots outside any short-circuit: under `||` the second one would count
                     // only the lanes that reach it)
-                    const unsigned long long gm = __ballot(tp && fam == 1), pm2 = __ballot(tp && fam == 2);
+                    const unsigned long long gm = __ballot(tp && fam == 1);
+#ifdef ARTES_DEBUG_LANES
+                    const unsigned long long pm2 = __ballot(tp && fam == 2);
+#endif
                     {
                         bool run = tp && fam == 2;
                         if (gm) {
