@@ -894,15 +894,17 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.emit_first = (int)tv(g, T_EMIT_FIRST, grid3d ? 0 : 1);
     R.backward = (int)tv(g, T_BACKWARD, 1);
     // lanes that park for the batched forced first interaction (kernel_trace.hpp): run the
-    // block once this many wait, or once fewer than batch_min lanes still step
-    R.batch = (int)tv(g, T_BATCH, 1);
+    // block once this many wait, or once fewer than batch_min lanes still step (2 since the
+    // common set-up block: ray3d +0.5 %, cloudy +0.3 %, hg / iso +0.2 %; 1 before,
+    // profiles/r05/ab/knobs_batch_hbatch.txt)
+    R.batch = (int)tv(g, T_BATCH, 2);
     // (>= 1: a wave whose stepping lanes all wait for a batch must run it)
     R.batch_min = (int)tv(g, T_BATCH_MIN, 16);
     // lanes whose propagation reached its interaction point park the same way: the
-    // interaction block (roulette, albedo weight, peel-off set-up) runs once this many wait
-    // (6 on 3D grids, where the block also computes the peel-off trace's set-up bounds; 4 on
-    // radial-only ones; profiles/r02/refill_hbatch_sweep*.txt)
-    R.hbatch = (int)tv(g, T_HBATCH, grid3d ? 6 : 4);
+    // interaction block (roulette, albedo weight) runs once this many wait: 4 (3D grids had 6
+    // while the block also set up the peel-off traces, which the common set-up block does
+    // now: ray3d +0.3 % at 4, cloudy the same; profiles/r05/ab/knobs_batch_hbatch.txt)
+    R.hbatch = (int)tv(g, T_HBATCH, 4);
     // trace-relative kernels: a lane whose nearest entry is a theta / phi bound waits until
     // this many lanes of the wave need that evaluation (or few lanes still step), so the
     // wave runs the theta / phi form in fewer iterations
