@@ -286,7 +286,7 @@ __device__ __forceinline__ TraceCursor load_cursor(const TraceCursor* p) {
 template <bool LA = false>
 __device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, int home, bool need, int grab, int* slot = nullptr,
                                          int* ck_cur = nullptr, int* ck_nxt = nullptr, const Lists* L = nullptr, int split = 0,
-                                         const Slot* rec = nullptr, unsigned lds_sink = 0) {
+                                         const Slot* rec = nullptr, unsigned lds_sink = 0, int* n_atom = nullptr) {
     constexpr int PF = 32;
     const int lane = threadIdx.x & 63;
     const unsigned long long mask = __ballot(need);
@@ -345,6 +345,7 @@ __device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, 
         const int req = max(want, grab);
         unsigned int base = 0;
         if (lane == 0) base = atomicAdd(&cursors[sh], (unsigned int)req);
+        if (n_atom) ++*n_atom;   // (timing build: the grabs a take issued)
         base = __builtin_amdgcn_readlane(base, 0);   // (uniform: an SGPR)
         const long long start = (long long)lo + base;
         const int all = (int)max(0LL, min((long long)req, (long long)hi - start));

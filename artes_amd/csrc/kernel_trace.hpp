@@ -582,9 +582,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         }
     }
 #ifdef ARTES_DEBUG_TIMING
-    __shared__ unsigned long long s_tm[BLOCK / 64][16];
+    __shared__ unsigned long long s_tm[BLOCK / 64][20];
     unsigned long long* const my_tm = s_tm[threadIdx.x >> 6];
-    if ((threadIdx.x & 63) < 16) my_tm[threadIdx.x & 63] = 0;
+    if ((threadIdx.x & 63) < 20) my_tm[threadIdx.x & 63] = 0;
     __builtin_amdgcn_wave_barrier();
     auto tm_tick = [&]() -> unsigned long long {
         __builtin_amdgcn_sched_barrier(0);
@@ -931,9 +931,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     my = wave_take<true>(cur, L.grab, home, !have, R.dgrab, &sl, &ck_cur, &ck_nxt, &L, split, S.s, pf_sink);
                     if (!have && my >= 0) slot = sl != -2 ? sl : L.trace_in[list_pos(my, split, L.P)];
                 } else {
+#ifdef ARTES_DEBUG_TIMING
+                    int n_atom = 0;
+                    my = wave_take(cur, L.grab, home, !have, R.dgrab, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0, &n_atom);
+#else
                     my = wave_take(cur, L.grab, home, !have, R.dgrab);
+#endif
                     TM_TICK(tr_b);
                     TM_ADD(9, tr_b - tr_a);
+#ifdef ARTES_DEBUG_TIMING
+                    // takes that issued dynamic grabs (atomics): their cycles, their count; all takes; grabs
+                    if (n_atom) { TM_ADD(16, tr_b - tr_a); TM_ADD(17, 1); }
+                    TM_ADD(18, 1);
+                    TM_ADD(19, n_atom);
+#endif
                     if (!have && my >= 0) slot = L.trace_in[list_pos(my, split, L.P)];
 #ifdef ARTES_DEBUG_TIMING
                     asm volatile("" ::"v"(slot));   // (the list entry's wait inside this region)
@@ -1550,7 +1561,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         TM_TICK(t_end);
         TM_ADD(7, t_end - t_begin);
         __builtin_amdgcn_wave_barrier();
-        if ((threadIdx.x & 63) < 16) atomicAdd(&R.err[threadIdx.x & 63], my_tm[threadIdx.x & 63]);
+        if ((threadIdx.x & 63) < 20 && (threadIdx.x & 63) != 15) atomicAdd(&R.err[threadIdx.x & 63], my_tm[threadIdx.x & 63]);
     }
 #endif
 #ifdef ARTES_DEBUG_LANES

@@ -161,7 +161,7 @@ def _direction_cosine(alpha, beta, d, errs, clamp=None):
 
 
 def _num(alpha, beta, d):
-    """direction_cosine's num before its clamps (ARTES.f90:2010-2022)."""
+    """direction_cosine's num before its clamps (ARTES.f90:1995-2005)."""
     cto = d[2] / math.sqrt(d[0] ** 2 + d[1] ** 2 + d[2] ** 2)
     sto = math.sqrt(1.0 - cto * cto)
     cb = math.cos(2 * PI - beta) if PI <= beta < 2 * PI else math.cos(beta)
