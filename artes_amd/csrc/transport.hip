@@ -907,8 +907,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.hbatch = (int)tv(g, T_HBATCH, 4);
     // trace-relative kernels: a lane whose nearest entry is a theta / phi bound waits until
     // this many lanes of the wave need that evaluation (or few lanes still step), so the
-    // wave runs the theta / phi form in fewer iterations
-    R.gbatch = (int)tv(g, T_GBATCH, coarse3d ? 8 : 4);
+    // wave runs the theta / phi form in fewer slots.  Fine 3D grids: no wait
+    // since the radial-form slots (1: ray3d k_trace -3.5 % against 4); coarse ones keep 8 (2:
+    // cloudy -2.3 %; profiles/r05/ab/knobs_gbatch*.txt)
+    R.gbatch = (int)tv(g, T_GBATCH, coarse3d ? 8 : 1);
     // the least list entries a dynamic grab of k_trace asks for (the wave keeps the rest for
     // its next refills; kernel_event.hpp, wave_take): 128 (profiles/r04/ab/dyn_grab_sweep*.txt)
     R.dgrab = (int)tv(g, T_DGRAB, 128);
