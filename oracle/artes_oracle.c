@@ -6,14 +6,17 @@
  * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.
  * The product path (artes_amd/, libartes_hip.so) never links or calls this file.
  *
- * Parity pinning: the reference has no tests or golden vectors and
- * cannot be rebuilt under this pipeline's rules (it needs cfitsio, which ships in
- * the reference only as a prebuilt binary, plus a stand-in for the GNU STAT
- * intrinsic).  This restatement is pinned (tests/test_oracle.py) against
+ * PARITY UNPINNED against the reference itself.  The reference has no tests or
+ * golden vectors and cannot be rebuilt under this pipeline's rules (it
+ * needs cfitsio, which ships in the reference only as a prebuilt binary, plus a
+ * stand-in for the GNU STAT intrinsic).  This restatement is checked
+ * (tests/test_oracle.py) against
  *   (a) analytic known-answer tests (single-scattering limit, energy normalisation,
  *       isotropic Q=U=V=0, Rayleigh polarisation at 90 degrees), and
- *   (b) frozen reference outputs produced when the survey ran the reference
- *       (tests/golden/, provenance in tests/golden/README.md),
+ *   (b) frozen outputs the survey produced by running a build of the reference with
+ *       that STAT stand-in, linked to the reference's prebuilt cfitsio (tests/golden/,
+ *       provenance in tests/golden/README.md) -- by this pipeline's rules such a build
+ *       pins nothing, so (b) is a consistency check, not a pin,
  * statistically, within the Monte-Carlo sigma the reference itself reports.
  *
  * Deliberate differences from the Fortran, all documented in DESIGN.md:
