@@ -1112,22 +1112,26 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 // C. Theta / phi (3D grids): the blocking family when it is one of them (a lane whose
                 // radial entry is still pending runs A again in its next step) -- the nearest pending
                 // bound first (w), or the lowest pending family when nothing lies beyond 1e-9 m.
-                // Theta evaluations (the quadratic from the current point) are batched: a lane that
+                // Theta evaluations (the quadratic from the current point) are batched in the
+                // 4-step kernel (coarse grids: short traces, many set-up evaluations): a lane that
                 // needs one waits until R.gbatch lanes of the wave do, or few lanes still step.
+                // The 8-step kernel evaluates at once (waiting measured 3.5 % slower on ray3d), with
+                // no ballots or counts (k_trace -2 %; profiles/r05/ab/trace_theta_unbatched_*).
                 if constexpr (G3D) {
+                    constexpr bool TBATCH = NREP < 8;
                     const bool tp = blocked && !(pending & 1);
-                    const unsigned long long act = __ballot(true);
-                    if (__ballot(tp)) {   // (a wave-uniform test first: ~10 % of the steps need this)
+                    [[maybe_unused]] const unsigned long long act = TBATCH ? __ballot(true) : 0;
+                    if (!TBATCH || __ballot(tp)) {   // (a wave-uniform test first: ~10 % of the steps need this)
                     const int fam = fast ? w : __builtin_ctz(pending & 6);
                     // (both ballots outside any short-circuit: under `||` the second one would count
                     // only the lanes that reach it)
-                    const unsigned long long gm = __ballot(tp && fam == 1);
+                    [[maybe_unused]] const unsigned long long gm = TBATCH ? __ballot(tp && fam == 1) : 0;
 #ifdef ARTES_DEBUG_LANES
                     const unsigned long long pm2 = __ballot(tp && fam == 2);
 #endif
                     {
-                        bool run = tp && fam == 2;
-                        if (gm) {
+                        bool run = TBATCH ? (tp && fam == 2) : tp;
+                        if (TBATCH && gm) {
                             const int ng = __popcll(gm);
                             const bool go = ng >= R.gbatch || __popcll(act) - ng < R.batch_min || exhausted;
                             run = run || (tp && fam == 1 && go);

@@ -111,7 +111,7 @@ static const TuneSpec TUNE[T_NUM] = {
     {"batch", 1, 64},            // batched forced first interaction: lanes that wait
     {"batch_min", 1, 64},        // ... or fewer than this many lanes still step
     {"hbatch", 1, 64},           // batched interaction + peel set-up: lanes that wait
-    {"gbatch", 1, 64},           // batched theta evaluations: lanes that wait
+    {"gbatch", 1, 64},           // batched theta evaluations: lanes that wait (the 4-step k_trace)
     {"defer", 1, 64},            // persistent engine: event deferral
     {"backward", 0, 1},          // backward walk after the forced first interaction
     {"emit_first", 0, 1},        // trace-list order
@@ -907,10 +907,11 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.hbatch = (int)tv(g, T_HBATCH, 4);
     // trace-relative kernels: a lane whose nearest entry is a theta / phi bound waits until
     // this many lanes of the wave need that evaluation (or few lanes still step), so the
-    // wave runs the theta / phi form in fewer slots.  Fine 3D grids: no wait
-    // since the radial-form slots (1: ray3d k_trace -3.5 % against 4); coarse ones keep 8 (2:
-    // cloudy -2.3 %; profiles/r05/ab/knobs_gbatch*.txt)
-    R.gbatch = (int)tv(g, T_GBATCH, coarse3d ? 8 : 1);
+    // wave runs the theta / phi form in fewer slots.  Only the 4-step kernel
+    // (coarse grids, or steps = 4) batches: 8 there (2: cloudy -2.3 %); the 8-step kernel
+    // evaluates at once since the radial-form slots (waiting for 4 measured 3.5 % slower on
+    // ray3d; profiles/r05/ab/knobs_gbatch*.txt)
+    R.gbatch = (int)tv(g, T_GBATCH, 8);
     // the least list entries a dynamic grab of k_trace asks for (the wave keeps the rest for
     // its next refills; kernel_event.hpp, wave_take): 128 (profiles/r04/ab/dyn_grab_sweep*.txt)
     R.dgrab = (int)tv(g, T_DGRAB, 128);
