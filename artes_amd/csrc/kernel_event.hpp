@@ -585,11 +585,38 @@ struct TabLayout {
     static constexpr int CUM = (NANG + 1) * CS;         // doubles per cumulative table
 };
 
+// Development timing build (-DARTES_DEBUG_TIMING): shader-clock cycles of k_event's regions,
+// summed per wave (its first active lane) into `ev_tm` (LDS) and added to error slots 20-27 at
+// the end of the kernel (the run's error codes are void): 20 the latch copy (the wait for the
+// prefetched record), 21 the whole event, 22 the peel, 23 the angle sampling, 24 the rest of the
+// scattering (direction, matrix, rotation, record writes), 25 list writes after the event,
+// 26 events, 27 the loop total (tools/time_regions.py)
+#ifdef ARTES_DEBUG_TIMING
+__device__ __forceinline__ unsigned long long ev_tick() {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = __builtin_readcyclecounter();
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+__device__ __forceinline__ void ev_add(unsigned long long* tm, int k, unsigned long long d) {
+    if ((int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) tm[k] += d;
+}
+#define EV_TICK(v) const unsigned long long v = ev_tick()
+#define EV_ADD(k, d) ev_add(ev_tm, k, d)
+#else
+#define EV_TICK(v)
+#define EV_ADD(k, d)
+#endif
+
 // one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended); the peel
 // contribution goes to `D` (see DetAcc)
 template <bool PIX1, bool PAD, bool PADC = PAD>
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, const Line0& L0,
-                                         DetAcc<PIX1>& D, uint32_t& c_scat, uint32_t& c_det) {
+                                         DetAcc<PIX1>& D, uint32_t& c_scat, uint32_t& c_det
+#ifdef ARTES_DEBUG_TIMING
+                                         , unsigned long long* ev_tm
+#endif
+                                         ) {
     {
         double* __restrict__ det = D.det;
         const size_t plane = D.plane;
@@ -618,6 +645,7 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         double cpo, spo;
         azimuth_cs(dx, dy, cpo, spo);
         bool drop = false;
+        EV_TICK(tp0);
         if ((m & FLAG_EXIT) && tau_peel < 50.0) {
             const double w = exp(-tau_peel);
             double mu = dx * R.det0 + dy * R.det1 + dz * R.det2;
@@ -671,6 +699,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
                 }
             }
         }
+        EV_TICK(tp1);
+        EV_ADD(22, tp1 - tp0);
         if (drop) { S.s[slot].mode = S_END_DROP; return 2; }
         // scatter_photon + polarization_rotation (ARTES.f90:819-846)
         c_scat++;
@@ -678,6 +708,11 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
         Rng rng; rng.s0 = L0.r0; rng.s1 = L0.r1;
         double alpha, beta, c2b, s2b, adeg;
         sample_angles<TC::CS>(G, R, G.cums + (size_t)mid * TC::CUM, rng, st, alpha, beta, c2b, s2b, &adeg);
+#ifdef ARTES_DEBUG_TIMING
+        asm volatile("" ::"v"(alpha), "v"(beta));   // (the sampling's result: its waits inside the region)
+#endif
+        EV_TICK(tp2);
+        EV_ADD(23, tp2 - tp1);
         double e0, e1, e2;
         direction_cosine_cs(R, alpha, beta, dx, dy, dz, cpo, spo, e0, e1, e2);
         // the matrix at the sampled angle itself (degrees), not at acos(cos(angle)) (ARTES.f90:
@@ -694,6 +729,8 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
             const double xi = rng.uni();
             S.s[slot].r0 = rng.s0; S.s[slot].r1 = rng.s1;
             start_prop(S, slot, -log(1.0 - xi));
+            EV_TICK(tp3);
+            EV_ADD(24, tp3 - tp2);
             return 1;
         } else {
             log_err(R, 50);
@@ -797,6 +834,13 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
     int slot_n = i + stride < n ? L.event[i + stride] : -1;
     Line0 cur;
     if (EV_PREFETCH && slot >= 0) cur = *(const Line0*)(S.s + slot);
+#ifdef ARTES_DEBUG_TIMING
+    __shared__ unsigned long long s_evtm[EB / 64][32];
+    unsigned long long* const ev_tm = s_evtm[threadIdx.x >> 6];
+    if ((threadIdx.x & 63) < 32) ev_tm[threadIdx.x & 63] = 0;
+    __builtin_amdgcn_wave_barrier();
+#endif
+    EV_TICK(tl0);
     for (; i < n_pad; i += stride) {
         const int slot_nn = i + 2 * stride < n ? L.event[i + 2 * stride] : -1;
         Line0 nxt;
@@ -808,7 +852,15 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
 #ifdef ARTES_DEBUG
         if (i < n) dbg_claim(R, L, slot, S.P, 1, slot >= 0 && to_event_list(cur.mode));
 #endif
+        EV_TICK(te0);
+#ifdef ARTES_DEBUG_TIMING
+        const int dest = slot >= 0 ? event_one<PIX1, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det, ev_tm) : 0;
+#else
         const int dest = slot >= 0 ? event_one<PIX1, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
+#endif
+        EV_TICK(te1);
+        EV_ADD(21, te1 - te0);
+        EV_ADD(26, 1);
         // the next propagation trace goes to the same position of the output trace list
         // (a hole, -1, for a dropped packet): no list-counter atomic, coalesced stores
 #ifdef ARTES_DEBUG
@@ -818,10 +870,23 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         if (i < n) L.trace_out[R.emit_first ? L.P - 1 - i : i] = (dest == 1) ? slot : -1;
 #endif
         wave_append(dest == 2, emit_entry(slot, S_END_DROP), L.emit, L.emit_n);   // (event_one set S_END_DROP)
+        EV_TICK(te2);
+        EV_ADD(25, te2 - te1);
         slot = slot_n;
         slot_n = slot_nn;
         if constexpr (EV_PREFETCH) cur = nxt;
+#ifdef ARTES_DEBUG_TIMING
+        asm volatile("" ::"v"(cur.px), "v"(cur.mode), "v"(cur.q3), "v"(cur.r0));   // (the copy's wait inside the region)
+#endif
+        EV_TICK(te3);
+        EV_ADD(20, te3 - te2);
     }
+    EV_TICK(tl1);
+    EV_ADD(27, tl1 - tl0);
+#ifdef ARTES_DEBUG_TIMING
+    __builtin_amdgcn_wave_barrier();
+    if ((threadIdx.x & 63) >= 20 && (threadIdx.x & 63) < 28) atomicAdd(&R.err[threadIdx.x & 63], ev_tm[threadIdx.x & 63]);
+#endif
     D.flush_wave();
     if constexpr (LDS_D) {
         __syncthreads();

@@ -39,7 +39,7 @@ for env in variants:
     g.kernel_times()
     r = g.run(p, 0, n, 2024)
     kt = g.kernel_times()
-    e = [int(r.err[k]) for k in range(20)]
+    e = [int(r.err[k]) for k in range(28)]
     total, iters = e[7], max(e[6], 1)
     C = r.counter("crossings")
     print(f"{name} {env}: {g.last_kernel_ms():.1f} ms, k_trace {kt['trace'][0]:.1f} ms, wave-iterations {iters:.3e}, "
@@ -55,6 +55,11 @@ for env in variants:
             ("  of the refill: trace set-up", e[12]), ("  of the evaluation: the batched theta form", e[5])]
     for lab, v in subs:
         print(f"    {lab:62s} {v / total:6.3f}  ({v / iters:7.0f} cycles per iteration)")
+    if e[27]:   # k_event's regions (kernel_event.hpp, ev_tick)
+        ev = e[27]
+        print(f"  k_event: {e[26]:.3e} wave-events, {ev / max(e[26], 1):.0f} wave cycles per event: latch copy (the prefetched "
+              f"record's wait) {e[20] / ev:.3f}, event {e[21] / ev:.3f} (peel {e[22] / ev:.3f}, angle sampling {e[23] / ev:.3f}, "
+              f"rest of the scattering {e[24] / ev:.3f}), list writes {e[25] / ev:.3f}")
     if e[18]:
         print(f"    takes: {e[18]:.3e}, of which with dynamic grabs {e[17]:.3e} ({e[19]:.3e} atomics); cycles per take "
               f"{e[9] / e[18]:.0f}, per take with grabs {e[16] / max(e[17], 1):.0f}, per take without "
