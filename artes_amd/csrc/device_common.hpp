@@ -11,7 +11,9 @@
 
 namespace artes {
 
-constexpr int NCOPY = 8;
+// privatised detector copies: up to NCOPY_MAX, copy = block index mod R.ncopy (a multiple of
+// 8, so one copy serves the blocks of one XCD); det_copies() picks how many (transport.hip)
+constexpr int NCOPY_MAX = 64;
 constexpr int BLOCK = 256;
 constexpr double PI = 3.14159265358979323846;
 constexpr double HALF_PI = PI / 2.0;
@@ -64,8 +66,9 @@ struct DevRun {
     double det_phi;                 // atan2(det1, det0) in [0, 2 pi] (peel_photon, ARTES.f90:4868-4870)
     double cdphi, sdphi;            // its cosine and sine
     double x_max, y_max, fstop, pmin, surface_albedo, theta_star, phi_star;
-    double* __restrict__ det;       // [NCOPY][4][4][ny][nx]
-    size_t det_stride;              // doubles per copy
+    double* __restrict__ det;       // [ncopy][4][4][ny][nx], copies det_stride doubles apart
+    size_t det_stride;              // doubles per copy (16 ny nx rounded up to 256 bytes)
+    int ncopy;                      // detector copies
     double* __restrict__ tot2;      // [CNT_COPIES][CNT_STRIDE] partials (tot_add) of: packet-level sum T^2 per Stokes, flux_emitted, flux_exit
     unsigned long long* __restrict__ cnt;   // [CNT_COPIES][CNT_STRIDE] partial counters (cnt_add), summed per call
     unsigned long long* __restrict__ err;   // [ARTES_NUM_ERR]
@@ -107,10 +110,10 @@ __device__ __forceinline__ void log_err(const DevRun& R, int code) { atomicAdd(&
 
 // The event counters are added once per wave at the end of every launch -- thousands of
 // same-address atomics per launch, which the memory side serialises -- so each block adds
-// into one of CNT_COPIES copies of them, 128 bytes apart (copy = block index mod 8, i.e.
-// its XCD), and the host's launch sums the copies into the caller's counters at the end
+// into one of CNT_COPIES copies of them, 256 bytes apart (copy = block index mod 64: eight
+// per XCD), and the host's launch sums the copies into the caller's counters at the end
 // of the call (sum_counters, transport.hip).
-constexpr int CNT_COPIES = 8, CNT_STRIDE = 16;
+constexpr int CNT_COPIES = 64, CNT_STRIDE = 32;
 __device__ __forceinline__ void cnt_add(const DevRun& R, int k, unsigned long long v) {
     atomicAdd(&R.cnt[(blockIdx.x % CNT_COPIES) * CNT_STRIDE + k], v);
 }

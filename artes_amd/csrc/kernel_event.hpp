@@ -117,6 +117,15 @@ constexpr int NSUB = 8;
 struct SubLists {
     Lists l[NSUB];
 };
+// The list counters and shard cursors each on a 256-byte line of their own: device-scope
+// atomics are performed at the memory side, and those on one line serialise there -- packed
+// [field][NSUB], the trace-out, event and emit counters of all 8 sub-engines and their 64 shard
+// cursors shared five lines.
+#ifndef ARTES_CNT_PAD
+#define ARTES_CNT_PAD 64
+#endif
+constexpr int CPAD = ARTES_CNT_PAD;   // ints from one counter (cursor) to the next
+__host__ __device__ constexpr int grab_at(int sub, int sh) { return (sub * 8 + sh) * CPAD; }
 __device__ __forceinline__ int sub_of_block() { return (int)blockIdx.x % NSUB; }
 __device__ __forceinline__ int sub_block() { return (int)blockIdx.x / NSUB; }
 __device__ __forceinline__ int sub_grid() { return (int)gridDim.x / NSUB; }
@@ -344,7 +353,7 @@ __device__ __forceinline__ int wave_take(TraceCursor& c, unsigned int* cursors, 
         const int want = k - got;
         const int req = max(want, grab);
         unsigned int base = 0;
-        if (lane == 0) base = atomicAdd(&cursors[sh], (unsigned int)req);
+        if (lane == 0) base = atomicAdd(&cursors[sh * CPAD], (unsigned int)req);
         if (n_atom) ++*n_atom;   // (timing build: the grabs a take issued)
         base = __builtin_amdgcn_readlane(base, 0);   // (uniform: an SGPR)
         const long long start = (long long)lo + base;
@@ -813,7 +822,7 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         G.mats = m; G.cums = c; G.sc2 = a; G.ss2 = b;
         lds_next = b + (NANG + 1);
     }
-    double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
+    double* __restrict__ det = R.det + (size_t)(blockIdx.x % R.ncopy) * R.det_stride;
     double* __restrict__ acc = det;
     if constexpr (LDS_D) {
         acc = lds_next;
@@ -1050,7 +1059,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
     const int out0 = R.emit_first ? 0 : *L.event_n;
     const unsigned long long pkt0 = *L.next_pkt;
     const size_t plane = (size_t)R.nx * R.ny;
-    double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
+    double* __restrict__ det = R.det + (size_t)(blockIdx.x % R.ncopy) * R.det_stride;
     uint32_t c_exit = 0, c_abs = 0, c_drop = 0, c_pkt = 0;
     double t2[4] = {0, 0, 0, 0};
     double f_emit = 0.0, f_exit = 0.0;   // thermal flux_emitted / flux_exit (ARTES.f90:607, 780, 953)
@@ -1212,7 +1221,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
 struct SubUse {
     int u[NSUB];
 };
-__global__ void k_init(Pool S, int* emit, int* emit_n /*[NSUB]*/, int Ps, SubUse use) {
+__global__ void k_init(Pool S, int* emit, int* emit_n /*[NSUB], CPAD apart*/, int Ps, SubUse use) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= Ps * NSUB) return;
     const int sub = i / Ps, j = i - sub * Ps;
@@ -1220,24 +1229,25 @@ __global__ void k_init(Pool S, int* emit, int* emit_n /*[NSUB]*/, int Ps, SubUse
         S.s[i].mode = S_FRESH;
         emit[i] = i;   // position j of sub-engine sub's emit list
     }
-    if (j == 0) emit_n[sub] = use.u[sub];
+    if (j == 0) emit_n[sub * CPAD] = use.u[sub];
 }
 
 // end of an iteration: the output trace list (k_event's event_n entries, then k_emit's
 // emit_n) becomes the input, the consumed input buffer is reset to become the next
 // output, packet ids advance by the emit-list length; event/emit lists and cursors are zeroed
-// (one block per sub-engine; counters are laid out [field][NSUB], see CNT_*)
+// (one block per sub-engine; counters are laid out [field][NSUB], CPAD ints apart: cnt_at)
 enum : int { CNT_IN0 = 0, CNT_IN1 = 1, CNT_EVENT = 2, CNT_EMIT = 3, CNT_SPLIT0 = 4, CNT_SPLIT1 = 5, CNT_DBG = 8, CNT_FIELDS = 16 };
+__host__ __device__ constexpr int cnt_at(int field, int sub) { return (field * NSUB + sub) * CPAD; }
 __global__ void k_rotate(int* cnt, int in, unsigned int* grab_all, unsigned long long* next_all, int emit_first, int P,
                          unsigned long long* err) {
     const int sub = blockIdx.x;
-    int* in_n = cnt + (CNT_IN0 + in) * NSUB + sub;
-    int* out_n = cnt + (CNT_IN0 + 1 - in) * NSUB + sub;
-    int* out_split = cnt + (CNT_SPLIT0 + 1 - in) * NSUB + sub;
-    int* event_n = cnt + CNT_EVENT * NSUB + sub;
-    int* emit_n = cnt + CNT_EMIT * NSUB + sub;
-    int* dbg_iter = cnt + CNT_DBG * NSUB + sub;
-    unsigned int* grab = grab_all + 8 * sub;
+    int* in_n = cnt + cnt_at(CNT_IN0 + in, sub);
+    int* out_n = cnt + cnt_at(CNT_IN0 + 1 - in, sub);
+    int* out_split = cnt + cnt_at(CNT_SPLIT0 + 1 - in, sub);
+    int* event_n = cnt + cnt_at(CNT_EVENT, sub);
+    int* emit_n = cnt + cnt_at(CNT_EMIT, sub);
+    int* dbg_iter = cnt + cnt_at(CNT_DBG, sub);
+    unsigned int* grab = grab_all + grab_at(sub, 0);
     unsigned long long* next_pkt = next_all + sub;
     (void)dbg_iter; (void)err;
     if (threadIdx.x == 0) {
@@ -1253,7 +1263,7 @@ __global__ void k_rotate(int* cnt, int in, unsigned int* grab_all, unsigned long
         *event_n = 0;
         *emit_n = 0;
     }
-    if (threadIdx.x < 8) grab[threadIdx.x] = 0;
+    if (threadIdx.x < 8) grab[threadIdx.x * CPAD] = 0;
 }
 
 }  // namespace artes

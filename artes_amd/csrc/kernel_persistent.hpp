@@ -13,7 +13,7 @@ template <bool G3D, bool TRACE>
 __global__ __launch_bounds__(BLOCK) void transport_kernel(DevGrid G, DevRun R) {
     const uint64_t nthreads = (uint64_t)gridDim.x * BLOCK;
     uint64_t next = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;   // static interleaved share
-    double* __restrict__ det = R.det + (size_t)(blockIdx.x % NCOPY) * R.det_stride;
+    double* __restrict__ det = R.det + (size_t)(blockIdx.x % R.ncopy) * R.det_stride;
     const size_t plane = (size_t)R.nx * R.ny;
 
     // per-lane packet-level moments and per-block counters live in LDS (they are touched

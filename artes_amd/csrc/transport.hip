@@ -15,8 +15,8 @@
 //
 // All arithmetic is FP64 (the reference is double precision; the cell-face quadratics
 // cancel ~15 digits at R ~ 7e7 m).  Tables: tables.hpp.  Detector: planes
-// 0-8 accumulated per k_event block in LDS and flushed into NCOPY privatised HBM copies
-// (copy = blockIdx % NCOPY), summed by reduce_detector.  No MFMA: this is branchy
+// 0-8 accumulated per k_event block in LDS and flushed into privatised HBM copies
+// (copy = blockIdx % ncopy, det_copies), summed by reduce_detector.  No MFMA: this is branchy
 // per-packet work, not a contraction.
 #include <hip/hip_runtime.h>
 
@@ -35,10 +35,6 @@
 
 namespace artes {
 
-// sum the NCOPY privatised detectors into `out` ([4][4][ny][nx], accumulated).  Copy
-// plane 8 counts the polarised peels, copy plane 9 the I-only ones (thermal emission,
-// surface): the reference adds the first to the counts of all four Stokes components
-// (ARTES.f90:4969-4972), the second to the count of I alone (4581, 4688)
 // add the CNT_COPIES partial event counters of a call (cnt_add) into the caller's counters
 __global__ void sum_counters(const unsigned long long* __restrict__ part, unsigned long long* __restrict__ out,
                              const double* __restrict__ tpart, double* __restrict__ tout) {
@@ -56,18 +52,30 @@ __global__ void sum_counters(const unsigned long long* __restrict__ part, unsign
     }
 }
 
-__global__ void reduce_detector(const double* __restrict__ copies, size_t stride, size_t plane, double* __restrict__ out) {
+// how many privatised detector copies a call uses: the blocks of a launch flush into them
+// with device-scope atomics, which the memory side serialises per line (a k_event block adds
+// its LDS detector at its end, a one-pixel wave its ten sums), so more copies, fewer blocks
+// per line: 64 while they fit in 64 MiB, at least 8
+static int det_copies(size_t stride) {
+    int n = NCOPY_MAX;
+    while (n > 8 && stride * n * sizeof(double) > ((size_t)64 << 20)) n >>= 1;
+    return n;
+}
+
+// sum the ncopy privatised detectors into `out` ([4][4][ny][nx], accumulated).  Copy
+// plane 8 counts the polarised peels, copy plane 9 the I-only ones (thermal emission,
+// surface): the reference adds the first to the counts of all four Stokes components
+// (ARTES.f90:4969-4972), the second to the count of I alone (4581, 4688)
+__global__ void reduce_detector(const double* __restrict__ copies, size_t stride, int ncopy, size_t plane, double* __restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= stride) return;
+    if (i >= 16 * plane) return;
     double s = 0.0;
-#pragma unroll
-    for (int c = 0; c < NCOPY; c++) s += copies[(size_t)c * stride + i];
+    for (int c = 0; c < ncopy; c++) s += copies[(size_t)c * stride + i];
     const size_t slot = i / plane;           // 0..15 = moment*4 + stokes
     if (slot == 8) {
         const size_t pix = i - 8 * plane;
         double s9 = 0.0;
-#pragma unroll
-        for (int c = 0; c < NCOPY; c++) s9 += copies[(size_t)c * stride + 9 * plane + pix];
+        for (int c = 0; c < ncopy; c++) s9 += copies[(size_t)c * stride + 9 * plane + pix];
         out[i] += s + s9;
         out[9 * plane + pix] += s;
         out[10 * plane + pix] += s;
@@ -164,9 +172,9 @@ struct artes_grid {
     int* d_lists[2] = {nullptr, nullptr};
     int* d_event = nullptr;
     int* d_emit = nullptr;
-    int* d_counts = nullptr;              // [0],[1] trace lists, [2] event, [3] emit, [4],[5] splits, [8] debug iteration
+    int* d_counts = nullptr;              // [field][NSUB], CPAD apart (cnt_at): [0],[1] trace lists, [2] event, [3] emit, [4],[5] splits, [8] debug iteration
     int* d_owner = nullptr;               // ARTES_DEBUG: [P] slot ownership tags
-    unsigned int* d_grab = nullptr;       // [8]
+    unsigned int* d_grab = nullptr;       // [NSUB][8] shard cursors, CPAD apart (grab_at)
     unsigned long long* d_next = nullptr;
     int* h_count = nullptr;               // pinned
     hipEvent_t ev_poll = nullptr;
@@ -272,10 +280,10 @@ int32_t artes_abi_version(void) { return ARTES_ABI_VERSION; }
 
 const char* artes_build_info(void) {
 #ifdef ARTES_DEV_KNOBS
-    return "artes_amd transport engine: gfx950 HIP, FP64, event engine (k_trace / k_event / k_emit), NCOPY=8; "
+    return "artes_amd transport engine: gfx950 HIP, FP64, event engine (k_trace / k_event / k_emit); "
            "development build: tuning also from ARTES_* environment variables";
 #else
-    return "artes_amd transport engine: gfx950 HIP, FP64, event engine (k_trace / k_event / k_emit), NCOPY=8";
+    return "artes_amd transport engine: gfx950 HIP, FP64, event engine (k_trace / k_event / k_emit)";
 #endif
 }
 
@@ -497,8 +505,8 @@ static int32_t ensure_pool(artes_grid* g, uint64_t n) {
     HIP_TRY(hipMalloc((void**)&g->d_owner, (size_t)P * sizeof(int)));
 #endif
     if (!g->d_counts) {
-        HIP_TRY(hipMalloc((void**)&g->d_counts, CNT_FIELDS * NSUB * sizeof(int)));
-        HIP_TRY(hipMalloc((void**)&g->d_grab, 8 * NSUB * sizeof(unsigned int)));
+        HIP_TRY(hipMalloc((void**)&g->d_counts, CNT_FIELDS * NSUB * CPAD * sizeof(int)));
+        HIP_TRY(hipMalloc((void**)&g->d_grab, 8 * NSUB * CPAD * sizeof(unsigned int)));
         HIP_TRY(hipMalloc((void**)&g->d_next, NSUB * sizeof(unsigned long long)));
         HIP_TRY(hipHostMalloc((void**)&g->h_count, 64, hipHostMallocDefault));
         HIP_TRY(hipEventCreateWithFlags(&g->ev_poll, hipEventDisableTiming));
@@ -556,8 +564,8 @@ static void launch_trace_any(artes_grid* g, int wpe, int steps, int bpc, const D
 static void dump_live(artes_grid* g, const int* cnt, int in, hipStream_t stream) {
     const int P = g->pool.P, Ps = P / NSUB;
     int n[NSUB], split[NSUB];
-    if (hipMemcpyAsync(n, cnt + (CNT_IN0 + in) * NSUB, sizeof(n), hipMemcpyDeviceToHost, stream) != hipSuccess) return;
-    if (hipMemcpyAsync(split, cnt + (CNT_SPLIT0 + in) * NSUB, sizeof(split), hipMemcpyDeviceToHost, stream) != hipSuccess) return;
+    if (hipMemcpy2DAsync(n, sizeof(int), cnt + cnt_at(CNT_IN0 + in, 0), CPAD * sizeof(int), sizeof(int), NSUB, hipMemcpyDeviceToHost, stream) != hipSuccess) return;
+    if (hipMemcpy2DAsync(split, sizeof(int), cnt + cnt_at(CNT_SPLIT0 + in, 0), CPAD * sizeof(int), sizeof(int), NSUB, hipMemcpyDeviceToHost, stream) != hipSuccess) return;
     if (hipStreamSynchronize(stream) != hipSuccess) return;
     for (int s = 0; s < NSUB; s++) {
         fprintf(stderr, "[artes] sub-engine %d: live trace list %d entries (split %d)\n", s, n[s], split[s]);
@@ -588,8 +596,8 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     int32_t rc = ensure_pool(g, R.n);
     if (rc) return rc;
     const int P = g->pool.P, Ps = P / NSUB;
-    HIP_TRY(hipMemsetAsync(g->d_counts, 0, CNT_FIELDS * NSUB * sizeof(int), stream));
-    HIP_TRY(hipMemsetAsync(g->d_grab, 0, 8 * NSUB * sizeof(unsigned int), stream));
+    HIP_TRY(hipMemsetAsync(g->d_counts, 0, CNT_FIELDS * NSUB * CPAD * sizeof(int), stream));
+    HIP_TRY(hipMemsetAsync(g->d_grab, 0, 8 * NSUB * CPAD * sizeof(unsigned int), stream));
     HIP_TRY(hipMemsetAsync(g->d_next, 0, NSUB * sizeof(unsigned long long), stream));
     if (g->d_owner) HIP_TRY(hipMemsetAsync(g->d_owner, 0xFF, (size_t)P * sizeof(int), stream));   // tags -1: unclaimed
     int* cnt = g->d_counts;
@@ -664,13 +672,13 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         for (int s = 0; s < NSUB; s++) {
             Lists& L = SL.l[s];
             const size_t o = (size_t)s * Ps, ot = (size_t)s * 2 * Ps;
-            L.trace_in = g->d_lists[in] + ot; L.trace_in_n = cnt + (CNT_IN0 + in) * NSUB + s;
-            L.trace_in_split = cnt + (CNT_SPLIT0 + in) * NSUB + s;
-            L.trace_out = g->d_lists[1 - in] + ot; L.trace_out_n = cnt + (CNT_IN0 + 1 - in) * NSUB + s;
-            L.event = g->d_event + o; L.event_n = cnt + CNT_EVENT * NSUB + s;
-            L.emit = g->d_emit + o; L.emit_n = cnt + CNT_EMIT * NSUB + s;
-            L.grab = g->d_grab + 8 * s; L.next_pkt = g->d_next + s;
-            L.dbg_owner = g->d_owner; L.dbg_iter = cnt + CNT_DBG * NSUB + s;
+            L.trace_in = g->d_lists[in] + ot; L.trace_in_n = cnt + cnt_at(CNT_IN0 + in, s);
+            L.trace_in_split = cnt + cnt_at(CNT_SPLIT0 + in, s);
+            L.trace_out = g->d_lists[1 - in] + ot; L.trace_out_n = cnt + cnt_at(CNT_IN0 + 1 - in, s);
+            L.event = g->d_event + o; L.event_n = cnt + cnt_at(CNT_EVENT, s);
+            L.emit = g->d_emit + o; L.emit_n = cnt + cnt_at(CNT_EMIT, s);
+            L.grab = g->d_grab + grab_at(s, 0); L.next_pkt = g->d_next + s;
+            L.dbg_owner = g->d_owner; L.dbg_iter = cnt + cnt_at(CNT_DBG, s);
             L.P = 2 * Ps; L.first = sub_first[s]; L.n = sub_n[s];
         }
         return SL;
@@ -683,7 +691,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     SubUse use;
     for (int s = 0; s < NSUB; s++) use.u[s] = (int)std::min<uint64_t>((uint64_t)Ps, std::max<uint64_t>(sub_n[s], 1));
     timed(g, ARTES_K_AUX, stream, [&] {
-        hipLaunchKernelGGL(k_init, dim3(((size_t)P + 255) / 256), dim3(256), 0, stream, g->pool, g->d_emit, cnt + CNT_EMIT * NSUB, Ps, use);
+        hipLaunchKernelGGL(k_init, dim3(((size_t)P + 255) / 256), dim3(256), 0, stream, g->pool, g->d_emit, cnt + cnt_at(CNT_EMIT, 0), Ps, use);
     });
     // pre-iteration: fill the pool; emitted packets go to trace list 0
     {
@@ -755,7 +763,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
             // (and the watchdog counter: a schedule bug fails the run at once instead of
             // every launch spinning to the watchdog)
             unsigned long long* h_wd = (unsigned long long*)(g->h_count + NSUB);
-            HIP_TRY(hipMemcpyAsync(g->h_count, cnt + (CNT_IN0 + in) * NSUB, NSUB * sizeof(int), hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipMemcpy2DAsync(g->h_count, sizeof(int), cnt + cnt_at(CNT_IN0 + in, 0), CPAD * sizeof(int), sizeof(int), NSUB, hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipMemcpyAsync(h_wd, R.err + ARTES_ERR_WATCHDOG, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipEventRecord(g->ev_poll, stream));
             HIP_TRY(hipEventSynchronize(g->ev_poll));
@@ -792,14 +800,15 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     if (p->nx < 1 || p->ny < 1 || (size_t)p->nx * p->ny > (1u << 26)) return fail(-22, "bad detector size");
     HIP_TRY(hipSetDevice(g->device));
     const size_t plane = (size_t)p->nx * p->ny;
-    const size_t stride = 16 * plane;
-    if (g->copies_cap < stride * NCOPY) {
+    const size_t stride = (16 * plane + 31) & ~(size_t)31;   // (copies on 256-byte lines of their own)
+    const int ncopy = det_copies(stride);
+    if (g->copies_cap < stride * ncopy) {
         if (g->d_copies) hipFree(g->d_copies);
         g->d_copies = nullptr;
-        HIP_TRY(hipMalloc((void**)&g->d_copies, stride * NCOPY * sizeof(double)));
-        g->copies_cap = stride * NCOPY;
+        HIP_TRY(hipMalloc((void**)&g->d_copies, stride * ncopy * sizeof(double)));
+        g->copies_cap = stride * ncopy;
     }
-    HIP_TRY(hipMemsetAsync(g->d_copies, 0, stride * NCOPY * sizeof(double), stream));
+    HIP_TRY(hipMemsetAsync(g->d_copies, 0, stride * ncopy * sizeof(double), stream));
 
     DevGrid G;
     G.nr = T.nr; G.ntheta = T.ntheta; G.nphi = T.nphi; G.ncell = T.ncell; G.nmat = T.nmat;
@@ -913,8 +922,9 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // ray3d; profiles/r05/ab/knobs_gbatch*.txt)
     R.gbatch = (int)tv(g, T_GBATCH, 8);
     // the least list entries a dynamic grab of k_trace asks for (the wave keeps the rest for
-    // its next refills; kernel_event.hpp, wave_take): 128 (profiles/r04/ab/dyn_grab_sweep*.txt)
-    R.dgrab = (int)tv(g, T_DGRAB, 128);
+    // its next refills; kernel_event.hpp, wave_take): 64 since the shard cursors have lines of
+    // their own (cloudy +0.8 %, the rest the same as 128; profiles/r05/ab/pad_knobs.txt)
+    R.dgrab = (int)tv(g, T_DGRAB, 64);
     // statically dealt share of the trace list, in 1/64 (the rest is grabbed dynamically):
     // 32 on 3D grids, 24 on radial-only ones since the dynamic grabs ask for 128 entries
     // (48 / 40 before: each grab was an atomic round trip; profiles/r04/ab/dyn_grab_sweep2_static.txt)
@@ -929,7 +939,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.cdphi = cos(R.det_phi); R.sdphi = sin(R.det_phi);
     R.x_max = p->x_max; R.y_max = p->y_max; R.fstop = p->fstop; R.pmin = p->photon_minimum;
     R.surface_albedo = p->surface_albedo; R.theta_star = p->theta_star; R.phi_star = p->phi_star;
-    R.det = g->d_copies; R.det_stride = stride;
+    R.det = g->d_copies; R.det_stride = stride; R.ncopy = ncopy;
     R.tot2 = g->d_tot_part; R.cnt = g->d_cnt_part; R.err = err_out; R.rec = rec;
     HIP_TRY(hipMemsetAsync(g->d_cnt_part, 0, CNT_COPIES * CNT_STRIDE * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(g->d_tot_part, 0, CNT_COPIES * CNT_STRIDE * sizeof(double), stream));
@@ -967,9 +977,9 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     }
     HIP_TRY(hipEventRecord(g->ev1, stream));
     g->timed = true;
-    const int rb = (int)((stride + 255) / 256);
+    const int rb = (int)((16 * plane + 255) / 256);
     timed(g, ARTES_K_AUX, stream, [&] {
-        hipLaunchKernelGGL(reduce_detector, dim3(rb), dim3(256), 0, stream, (const double*)g->d_copies, stride, plane, det_out);
+        hipLaunchKernelGGL(reduce_detector, dim3(rb), dim3(256), 0, stream, (const double*)g->d_copies, stride, ncopy, plane, det_out);
         hipLaunchKernelGGL(sum_counters, dim3(1), dim3(64), 0, stream, (const unsigned long long*)g->d_cnt_part, cnt_out,
                            (const double*)g->d_tot_part, tot_out);
     });
