@@ -894,8 +894,10 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     // stay at 16; profiles/r04/ab/refill_after_trel.txt)
     // (with 4 steps per k_trace iteration on coarse 3D grids: 20 there, with theta batches of 8 --
     // the cloudy calls +1.8 %, two runs; profiles/r04/ab/cloudy_refill_gbatch_theta2.txt)
-    const bool coarse3d = grid3d && T.ncell < 4096;
-    R.refill = (int)tv(g, T_REFILL, grid3d ? (coarse3d ? 20 : 16) : 28);
+    // (round 5, with the counters on lines of their own, the takes are cheaper: 16 on all 3D
+    // grids -- the cloudy calls +0.4 % against 20 -- and 20 on radial-only ones -- hg +0.5 %,
+    // iso +0.2 % against 28; profiles/r05/ab/pad_refill.txt)
+    R.refill = (int)tv(g, T_REFILL, grid3d ? 16 : 20);
     // ended chains' list appends at the wave's next refill (kernel_trace.hpp `append`): ray3d
     // +3.7 %, hg +5.1 %, iso +2.7 %, the cloudy configs[3] calls +3.4-3.8 % (3e8 / 1e8 packets,
     // profiles/r03/late_append_ab.txt)
