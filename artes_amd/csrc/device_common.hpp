@@ -617,7 +617,11 @@ __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* _
     const double w = p12 * st[2] - p13 * st[1];
     auto cb = [&](int i) { return (double)i * u + v * G.sc2[i] + w * G.ss2[i]; };
     double s = rng.uni() * cb(180);
+#ifdef ARTES_SEARCH2
+    int i = cdf_search(s, cb);
+#else
     int i = cdf_search4(s, cb);
+#endif
     double y0 = cb(i - 1), y1 = cb(i);
     beta = (s - y0) / (y1 - y0) + (double)(i - 1);
     beta = beta * PI / 180.0;
@@ -632,7 +636,11 @@ __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* _
         return k0 * a[0] + k1 * a[1] + k2 * a[2] + k3 * a[3];
     };
     s = rng.uni() * ct(180);
+#ifdef ARTES_SEARCH2
+    i = cdf_search(s, ct);
+#else
     i = cdf_search4(s, ct);
+#endif
     y0 = ct(i - 1);
     y1 = ct(i);
     const double adeg = (s - y0) / (y1 - y0) + (double)(i - 1);
