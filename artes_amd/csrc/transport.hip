@@ -521,6 +521,10 @@ static int round_sub(int blocks) { return std::max(NSUB, (blocks + NSUB - 1) / N
 // albedo in LDS as well, for grids whose table fits, measured the same as reading them from
 // L2 -- cloudy 210.8 vs 211.1, hg 705 vs 707 Mpackets/s, profiles/r03/klds_ab.txt -- so they
 // stay in global memory.)
+// step slots per k_trace iteration of the `steps` = 4 kernel (A/B builds: ARTES_COARSE_NREP)
+#ifndef ARTES_COARSE_NREP
+#define ARTES_COARSE_NREP 4
+#endif
 template <bool G3D, bool OBL, int WPE, bool FLOW = false, int NREP = 8>
 static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L, hipStream_t stream) {
     const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
@@ -553,7 +557,7 @@ static void launch_trace_any(artes_grid* g, int wpe, int steps, int bpc, const D
     } else if (wpe == 3) {
         launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
     } else if (G3D && steps == 4) {
-        launch_trace<G3D, false, 4, false, 4>(g, bpc, G, R, L, stream);
+        launch_trace<G3D, false, 4, false, ARTES_COARSE_NREP>(g, bpc, G, R, L, stream);
     } else {
         launch_trace<G3D, false, 4>(g, bpc, G, R, L, stream);
     }
