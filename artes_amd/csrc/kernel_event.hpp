@@ -1067,7 +1067,13 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
     for (int i = sub_block() * BLOCK + threadIdx.x; i < n_pad; i += sub_grid() * BLOCK) {
         const int e = i < n ? L.emit[i] : -1;
         const int slot = e >= 0 ? (e & 0x07FFFFFF) : -1, code = e >= 0 ? (e >> 27) & 3 : 0;
+        // (code 0 is a fresh slot, (L3): its record is not read -- k_init leaves it unwritten
+        // outside the debug build, and this kernel writes the whole line before any use)
+#ifdef ARTES_DEBUG
         const int m = code ? S_END_EXIT - 1 + code : (slot >= 0 ? S.s[slot].mode : S_RETIRED);
+#else
+        const int m = code ? S_END_EXIT - 1 + code : (slot >= 0 ? (int)S_FRESH : (int)S_RETIRED);
+#endif
 #ifdef ARTES_DEBUG
         if (i < n) dbg_claim(R, L, slot, S.P, 2, (m == S_END_EXIT || m == S_END_ABS || m == S_END_DROP || m == S_FRESH) &&
                                                      (slot < 0 || S.s[slot].mode == m));
@@ -1226,7 +1232,9 @@ __global__ void k_init(Pool S, int* emit, int* emit_n /*[NSUB], CPAD apart*/, in
     if (i >= Ps * NSUB) return;
     const int sub = i / Ps, j = i - sub * Ps;
     if (j < use.u[sub]) {
-        S.s[i].mode = S_FRESH;
+#ifdef ARTES_DEBUG
+        S.s[i].mode = S_FRESH;   // (only the debug build's list checks read a fresh slot's mode)
+#endif
         emit[i] = i;   // position j of sub-engine sub's emit list
     }
     if (j == 0) emit_n[sub * CPAD] = use.u[sub];
