@@ -140,6 +140,24 @@ def test_zero_and_tiny_runs(require_gpu):
     assert r7.counter("packets") == 7
 
 
+def test_reused_pool_gives_fresh_results(require_gpu):
+    """A grid's packet pool outlives its calls, and k_init no longer rewrites the slot records
+    (kernel_event.hpp, k_init / k_emit: a fresh slot is known from its emit entry alone): a
+    call after larger and smaller ones on the same grid gives the counters of a fresh grid
+    and its detector to summation order."""
+    atm, grid, p = _setup("ray3d", nr=10, ntheta=6, nphi=8)
+    grid.run(p, 0, 200000, 11)
+    grid.run(p, 3, 5000, 12)
+    again = grid.run(p, 100, 60000, 13)
+    grid.close()
+    atm, fresh_grid, p = _setup("ray3d", nr=10, ntheta=6, nphi=8)
+    fresh = fresh_grid.run(p, 100, 60000, 13)
+    fresh_grid.close()
+    np.testing.assert_array_equal(again.counters, fresh.counters)
+    np.testing.assert_allclose(again.det, fresh.det, rtol=1e-9, atol=1e-300)
+    np.testing.assert_array_equal(again.err, fresh.err)
+
+
 def test_bench_line_contract(require_gpu):
     """bench.py (the driver's measurement) prints one JSON line with the contract's fields,
     on a small packet count (a subprocess: the bench owns its process)."""
