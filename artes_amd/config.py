@@ -80,11 +80,13 @@ class RunConfig:
     distance_planet: float = 10.0 * PC
     flow_global: bool = False
     flow_theta: bool = False
+    engine: dict = field(default_factory=dict)   # engine:<key>=<int> -- launch tuning (not a reference key)
     applied: list = field(default_factory=list)
 
     def copy(self) -> "RunConfig":
-        c = RunConfig(**{f.name: getattr(self, f.name) for f in fields(self) if f.name != "applied"})
+        c = RunConfig(**{f.name: getattr(self, f.name) for f in fields(self) if f.name not in ("applied", "engine")})
         c.applied = list(self.applied)
+        c.engine = dict(self.engine)
         return c
 
     # ------------------------------------------------------------------ keys
@@ -191,6 +193,19 @@ class RunConfig:
                 self.flow_theta = True
             elif v == "off":
                 self.flow_theta = False
+        elif k.startswith("engine:"):
+            # An extension of the reference's keyword table: engine:<tuning key>=<integer> passes an
+            # artes_set_tuning key of this engine to every grid the run creates (e.g.
+            # -k engine:det_ordered=1 for bit-reproducible detector images; include/artes_amd.h)
+            from .engine import TUNING_KEYS
+
+            name = k[len("engine:"):]
+            if name not in TUNING_KEYS:
+                raise ConfigError(f"Wrong keyword found in input file: {k}")
+            try:
+                self.engine[name] = int(v)
+            except ValueError:
+                raise ConfigError(f"Wrong value for {k}: {v}") from None
         else:
             raise ConfigError(f"Wrong keyword found in input file: {k}")
 

@@ -49,6 +49,7 @@ struct DevGrid {
     int th_ncdf, th_cd0;                 // CDF length; radial index of its first entry
     double th_total;
     double ox, oy, oz;                   // oblate_x, oblate_y, oblate_z (ARTES.f90:469-471)
+    double* ttab;                        // k_trace's face tables in global memory (GTAB kernels: tables beyond 64 KiB), or null
 };
 
 struct DevRun {
@@ -69,6 +70,9 @@ struct DevRun {
     double* __restrict__ det;       // [ncopy][4][4][ny][nx], copies det_stride doubles apart
     size_t det_stride;              // doubles per copy (16 ny nx rounded up to 256 bytes)
     int ncopy;                      // detector copies
+    unsigned long long* __restrict__ fix;   // det_ordered: [nfix][10][ny][nx] 128-bit fixed-point planes 0-9 (lo, hi), or null
+    size_t fix_stride;              // u64 per fixed-point copy (20 ny nx)
+    int nfix;                       // fixed-point copies (copy = block index mod nfix)
     double* __restrict__ tot2;      // [CNT_COPIES][CNT_STRIDE] partials (tot_add) of: packet-level sum T^2 per Stokes, flux_emitted, flux_exit
     unsigned long long* __restrict__ cnt;   // [CNT_COPIES][CNT_STRIDE] partial counters (cnt_add), summed per call
     unsigned long long* __restrict__ err;   // [ARTES_NUM_ERR]
@@ -302,6 +306,10 @@ __device__ __forceinline__ double dsqrt(double x) {
     return x > 0.0 ? g : (x == 0.0 ? x : __builtin_nan(""));
 }
 
+// the correctly rounded square root (as the reference's sqrt): where a rounding decides a branch
+// (direction_cosine_cs, peel_rotation)
+__device__ __forceinline__ double ref_sqrt(double x) { return __builtin_sqrt(x); }
+
 // mueller_matrix_filler (ARTES.f90:1934-1960): returns c2p, s2p
 __device__ __forceinline__ void mueller(double psi, double& c2p, double& s2p) {
     c2p = cos_b(2.0 * psi);
@@ -422,7 +430,11 @@ __device__ __forceinline__ bool peel_rotation(const DevRun& R, double dz, double
         log_err(R, 45);
         return false;
     }
-    const double num = (R.det2 - dz * mu) / (dsqrt(1.0 - mu * mu) * dsqrt(1.0 - dz * dz));
+    double num;
+    {   // (the reference's evaluation, as direction_cosine_cs's num)
+#pragma clang fp contract(off)
+        num = (R.det2 - dz * mu) / (ref_sqrt(1.0 - mu * mu) * ref_sqrt(1.0 - dz * dz));
+    }
     double x = 1.0;
     bool nan = false;
     if (fabs(num) < 1.0) x = num;
@@ -466,19 +478,30 @@ __device__ __forceinline__ void azimuth_cs(double d0, double d1, double& c, doub
 // of the angle.  The reference takes the sine as +-sqrt(1 - cos^2) by phi_new's half-turn,
 // the same value up to rounding (its sign is sin(phi_new)'s); the error paths keep their
 // phi_new = 0, i.e. (cos, sin) = (1, 0).
+//
+// The clamp of num at +-1 moves the azimuth by acos(1 - 1e-10) = 1.4e-5 rad on one side of it,
+// so which side num rounds to is a decision, not a rounding: where the new direction lies in
+// the old one's meridian plane (beta = 0 or pi) num is +-1 in exact arithmetic.  num and the
+// four values it is made of are therefore evaluated as the reference writes them -- its
+// operation order, no fused multiply-adds, correctly rounded square roots and division -- so
+// the device takes the reference's side of the clamp wherever its cosine of beta rounds alike
+// (tests/test_gpu_unit_checks.py, the boundary cases).
 __device__ void direction_cosine_cs(const DevRun& R, double alpha, double beta, double d0, double d1, double d2,
                                     double cpo, double spo, double& e0, double& e1, double& e2) {
-    const double cto = d2 / dsqrt(d0 * d0 + d1 * d1 + d2 * d2);
-    const double sto = dsqrt(1.0 - cto * cto);
-    double ctn = 0.0;
     const bool upper = (beta >= PI && beta < TWO_PI);
     const bool lower = (beta >= 0.0 && beta < PI);
     // (one cosine of the branch's argument: the same value, no divergent pair)
     const double cbeta = cos_b(upper ? TWO_PI - beta : beta);
-    if (upper || lower) ctn = cto * alpha + sto * dsqrt(1.0 - alpha * alpha) * cbeta;
-    else log_err(R, 18);
-    const double stn = dsqrt(1.0 - ctn * ctn);
-    double num = (alpha - ctn * cto) / (stn * sto);
+    double cto, sto, ctn = 0.0, stn, num;
+    {
+#pragma clang fp contract(off)
+        cto = d2 / ref_sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        sto = ref_sqrt(1.0 - cto * cto);
+        if (upper || lower) ctn = cto * alpha + sto * ref_sqrt(1.0 - alpha * alpha) * cbeta;
+        stn = ref_sqrt(1.0 - ctn * ctn);
+        num = (alpha - ctn * cto) / (stn * sto);
+    }
+    if (!(upper || lower)) log_err(R, 18);
     if (num >= 1.0) num = 1.0 - 1.e-10;
     else if (num <= -1.0) num = -1.0 + 1.e-10;
     double cpn = 1.0, spn = 0.0;

@@ -457,29 +457,63 @@ __device__ __forceinline__ int peel_pixel(const DevRun& R, double px, double py,
 // LDS slot (ten doubles, stride = the block size: conflict-free; registers would take the
 // kernel past 168 VGPRs, i.e. 2 waves per SIMD) -- and reduces them over the wave once, at
 // the end of the kernel (ARTES.f90:4953-4972 sums).
-template <bool PIX1>
+// Reproducible accumulation (tuning "det_ordered", DM_ORD): the floating-point sums above depend
+// on the order in which the dynamically scheduled events reach each address, so two identical
+// runs differ in the last bits.  Integer addition is associative: each contribution is rounded
+// once to a 128-bit fixed-point integer, round(|v| 2^80) with v's sign (resolution 2^-80 ~ 8e-25,
+// range 2^47; contributions are packet weights of order 1), and added with two 64-bit integer
+// atomics -- the low word with the old value returned, its carry into the high word -- so every
+// schedule ends with the same bits.  reduce_fixed sums the copies in integers and converts once.
+__device__ __forceinline__ void fix_add(unsigned long long* e, double v) {
+    const double a = fmin(fabs(v), 0x1p46) * 0x1p80;      // (exact scaling; |v| beyond 2^46 saturates)
+    const double hd = floor(a * 0x1p-64);
+    const double r = a - hd * 0x1p64;                      // (exact: a's bits below 2^64)
+    unsigned long long lo = (unsigned long long)rint(r), hi = (unsigned long long)(long long)hd;
+    if (v < 0.0) {   // two's complement of the 128-bit value
+        hi = ~hi + (lo == 0 ? 1ull : 0ull);
+        lo = 0ull - lo;
+    }
+    if ((lo | hi) == 0) return;
+    const unsigned long long old = atomicAdd(e, lo);
+    atomicAdd(e + 1, hi + (old + lo < old ? 1ull : 0ull));
+}
+
+// Detector accumulation of k_event: planes 0-8 (I Q U V sums, their squares, the peel
+// count) go to `acc` (the block's LDS detector or its HBM copy), plane 9 (the I-only peel
+// count) and the packet moments 12-15 to `det` (the block's HBM copy).  With a one-pixel
+// detector (spectrum / phase, ARTES.f90:453-465) every peel of the grid would add to the
+// same ten addresses, so PIX1 keeps per-lane partial sums instead -- in the lane's own
+// LDS slot (ten doubles, stride = the block size: conflict-free; registers would take the
+// kernel past 168 VGPRs, i.e. 2 waves per SIMD) -- and reduces them over the wave once, at
+// the end of the kernel (ARTES.f90:4953-4972 sums).  DM_ORD: planes 0-9 as fixed-point
+// integers in the block's copy of R.fix (fix_add).
+enum : int { DM_ATOM = 0, DM_PIX1 = 1, DM_ORD = 2 };
+template <int DM>
 struct DetAcc {
     double* __restrict__ det;
     double* __restrict__ acc;
     size_t plane;
     double* __restrict__ lane;   // PIX1: this lane's slot, lane[k * stride]
     int stride;
-    __device__ __forceinline__ void init(double* d, double* a, size_t pl, double* slots = nullptr, int nthreads = 0) {
-        det = d; acc = a; plane = pl;
-        if constexpr (PIX1) {
+    unsigned long long* __restrict__ fix;   // DM_ORD: the block's fixed-point copy
+    __device__ __forceinline__ void init(double* d, double* a, size_t pl, double* slots = nullptr, int nthreads = 0,
+                                         unsigned long long* f = nullptr) {
+        det = d; acc = a; plane = pl; fix = f;
+        if constexpr (DM == DM_PIX1) {
             lane = slots + threadIdx.x; stride = nthreads;
 #pragma unroll
             for (int k = 0; k < 10; k++) lane[k * stride] = 0.0;
         }
     }
     __device__ __forceinline__ void add(int k, int pix, double v) {
-        if constexpr (PIX1) lane[k * stride] += v;
+        if constexpr (DM == DM_PIX1) lane[k * stride] += v;
+        else if constexpr (DM == DM_ORD) fix_add(fix + 2 * ((size_t)k * plane + pix), v);
         else if (k == 9) unsafeAtomicAdd(&det[9 * plane + pix], v);   // rare (thermal / surface)
         else unsafeAtomicAdd(&acc[k * plane + pix], v);
     }
     // PIX1: one wave-reduced add per plane (call with the whole wave)
     __device__ __forceinline__ void flush_wave() {
-        if constexpr (PIX1) {
+        if constexpr (DM == DM_PIX1) {
 #pragma unroll
             for (int k = 0; k < 10; k++) {
                 const double v = wave_sum_f64(lane[k * stride]);
@@ -494,8 +528,8 @@ __host__ __device__ inline size_t pix1_slot_bytes(int block) { return (size_t)10
 
 // a peel that carries Stokes I only (peel_thermal 4577-4583, peel_surface 4684-4690):
 // moments 0 and 4, and the I-only count plane 9 (the reference counts it for I alone)
-template <bool PIX1>
-__device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int slot, DetAcc<PIX1>& D, double v, int err_code,
+template <int DM>
+__device__ __forceinline__ void add_peel_I(const DevRun& R, const Pool& S, int slot, DetAcc<DM>& D, double v, int err_code,
                                            uint32_t& c_det) {
     if (!(v > 0.0 && v < 1.e100)) { log_err(R, err_code); return; }
     const int pix = peel_pixel(R, S.s[slot].px, S.s[slot].py, S.s[slot].pz);
@@ -532,8 +566,8 @@ __device__ __forceinline__ void surface_normal(const DevGrid& G, double x, doubl
 
 // thermal-emission peel done (ARTES.f90:599-622, 4566-4591), then the first optical
 // depth trace of the packet; returns 1 (next trace) or 2 (dropped)
-template <bool PIX1>
-__device__ __forceinline__ int event_thermal(const DevRun& R, const Pool& S, int slot, DetAcc<PIX1>& D, uint32_t& c_det) {
+template <int DM>
+__device__ __forceinline__ int event_thermal(const DevRun& R, const Pool& S, int slot, DetAcc<DM>& D, uint32_t& c_det) {
     const int m = S.s[slot].mode;
     if (m & FLAG_ERR) { log_err(R, 47); S.s[slot].mode = S_END_DROP; return 2; }
     const double tau = S.s[slot].tpeel;
@@ -567,8 +601,8 @@ __device__ __forceinline__ int event_surface_hit(const DevGrid& G, const DevRun&
 }
 
 // surface peel done (ARTES.f90:4633-4700), then the interrupted propagation resumes
-template <bool PIX1>
-__device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S, int slot, DetAcc<PIX1>& D, uint32_t& c_det) {
+template <int DM>
+__device__ __forceinline__ int event_surface_peel(const DevRun& R, const Pool& S, int slot, DetAcc<DM>& D, uint32_t& c_det) {
     const int m = S.s[slot].mode;
     const double tau = S.s[slot].tpeel;
     if (!(m & FLAG_ERR) && (m & FLAG_EXIT) && tau < 50.0)
@@ -619,9 +653,9 @@ __device__ __forceinline__ void ev_add(unsigned long long* tm, int k, unsigned l
 
 // one peel-off + scattering event; returns 1 (next trace) or 2 (packet ended); the peel
 // contribution goes to `D` (see DetAcc)
-template <bool PIX1, bool PAD, bool PADC = PAD>
+template <int DM, bool PAD, bool PADC = PAD>
 __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, const Pool& S, int slot, const Line0& L0,
-                                         DetAcc<PIX1>& D, uint32_t& c_scat, uint32_t& c_det
+                                         DetAcc<DM>& D, uint32_t& c_scat, uint32_t& c_det
 #ifdef ARTES_DEBUG_TIMING
                                          , unsigned long long* ev_tm
 #endif
@@ -785,9 +819,13 @@ static constexpr bool EV_PREFETCH = ARTES_EV_PREFETCH != 0;
 //         event, then wait on LDS, and only the interpolation's independent row reads go to
 //         L2.  (The call's matrices are its wavelength's only: the host remaps matrix ids
 //         per wavelength, transport.hip, wl_set.)
-template <bool LDS_T, bool LDS_D, bool PIX1 = false, int EB = BLOCK, bool LDS_C = false>
+//  ORD:   planes 0-9 as 128-bit fixed-point integers (DetAcc DM_ORD; tuning "det_ordered"):
+//         bit-reproducible detector images, no LDS detector or per-lane sums.
+template <bool LDS_T, bool LDS_D, bool PIX1 = false, int EB = BLOCK, bool LDS_C = false, bool ORD = false>
 __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, SubLists SL) {
     static_assert(!(PIX1 && LDS_D), "a one-pixel detector is reduced per lane");
+    static_assert(!(ORD && (PIX1 || LDS_D)), "the ordered detector is accumulated in integers in HBM");
+    constexpr int DM = ORD ? DM_ORD : (PIX1 ? DM_PIX1 : DM_ATOM);
     static_assert(!(LDS_T && LDS_C), "LDS_C stages the cumulative tables alone");
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_ev[];
@@ -829,8 +867,8 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         for (size_t i = threadIdx.x; i < 9 * plane; i += EB) acc[i] = 0.0;
     }
     if constexpr (LDS_T || LDS_D || LDS_C) __syncthreads();
-    DetAcc<PIX1> D;
-    D.init(det, acc, plane, lds_next, EB);
+    DetAcc<DM> D;
+    D.init(det, acc, plane, lds_next, EB, ORD ? R.fix + (size_t)(blockIdx.x % R.nfix) * R.fix_stride : nullptr);
     const int n = *L.event_n;
     uint32_t c_scat = 0, c_det = 0;
     const int n_pad = (n + 63) & ~63;   // whole waves iterate together (wave-aggregated appends)
@@ -863,9 +901,9 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
 #endif
         EV_TICK(te0);
 #ifdef ARTES_DEBUG_TIMING
-        const int dest = slot >= 0 ? event_one<PIX1, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det, ev_tm) : 0;
+        const int dest = slot >= 0 ? event_one<DM, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det, ev_tm) : 0;
 #else
-        const int dest = slot >= 0 ? event_one<PIX1, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
+        const int dest = slot >= 0 ? event_one<DM, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
 #endif
         EV_TICK(te1);
         EV_ADD(21, te1 - te0);

@@ -161,14 +161,28 @@ struct TraceTabs {
     const double2* rr;    // (r_k, r_k+1): a radial shell's two radii (the trace-relative sphere roots)
 };
 
+// (rr has nr + 1 entries: the fused radial step reads rr[kn] for kn = -1 .. nr before it knows
+// whether the packet stays in the grid -- rr[-1] is the last tcs entry, rr[nr] a pad -- and uses
+// the values only when kn names a shell)
 __host__ __device__ inline size_t trace_table_bytes(int nr, int ntheta, int nphi) {
-    return sizeof(FaceRec) * ((size_t)(nr + 1) + (size_t)(ntheta + 1)) + sizeof(double2) * ((size_t)nphi + ntheta + 1 + nr);
+    return sizeof(FaceRec) * ((size_t)(nr + 1) + (size_t)(ntheta + 1)) + sizeof(double2) * ((size_t)nphi + ntheta + 1 + nr + 1);
 }
-__device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double* lds) {
+// The tables' layout from `base` (LDS, or the global copy of the GTAB kernels)
+__device__ __forceinline__ TraceTabs trace_tables_at(const DevGrid& G, double* base) {
     TraceTabs T;
-    FaceRec* fr = (FaceRec*)lds;
-    for (int i = threadIdx.x; i <= G.nr; i += BLOCK) fr[i] = FaceRec{1.0, G.rf2[i], 0.0, FR_KS_IN | FR_BIG_OUT, 0};
-    for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) {
+    FaceRec* fr = (FaceRec*)base;
+    double2* phsc = (double2*)(fr + (G.nr + 1) + (G.ntheta + 1));
+    double2* tcs = phsc + G.nphi;
+    double2* rr = tcs + G.ntheta + 1;
+    T.fr = fr; T.phsc = phsc; T.tcs = tcs; T.rr = rr;
+    return T;
+}
+// Fill the tables at `base`, thread `tid` of `nt`
+__device__ __forceinline__ void fill_trace_tables(const DevGrid& G, double* base, int tid, int nt) {
+    const TraceTabs T = trace_tables_at(G, base);
+    FaceRec* fr = (FaceRec*)T.fr;
+    for (int i = tid; i <= G.nr; i += nt) fr[i] = FaceRec{1.0, G.rf2[i], 0.0, FR_KS_IN | FR_BIG_OUT, 0};
+    for (int i = tid; i <= G.ntheta; i += nt) {
         const double th = G.thetaf[i];
         const bool cone = G.tplane[i] == 1;
         const double sg = cone ? (th > HALF_PI ? 1.0 : (th < HALF_PI ? -1.0 : 0.0)) : 0.0;
@@ -176,19 +190,27 @@ __device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double
                        ((i == 0 || i == G.ntheta) ? FR_EDGE : 0) | FR_BIG_OUT | FR_BIG_IN;
         fr[G.nr + 1 + i] = FaceRec{-G.tan2[i], 0.0, sg, fl, 0};
     }
-    double2* phsc = (double2*)(fr + (G.nr + 1) + (G.ntheta + 1));
-    for (int i = threadIdx.x; i < G.nphi; i += BLOCK) phsc[i] = make_double2(G.phis[i], G.phic[i]);
-    double2* tcs = phsc + G.nphi;
-    for (int i = threadIdx.x; i <= G.ntheta; i += BLOCK) {
+    double2* phsc = (double2*)T.phsc;
+    for (int i = tid; i < G.nphi; i += nt) phsc[i] = make_double2(G.phis[i], G.phic[i]);
+    double2* tcs = (double2*)T.tcs;
+    for (int i = tid; i <= G.ntheta; i += nt) {
         const double c = G.tcos[i];
         tcs[i] = make_double2(c, sqrt(fmax(0.0, 1.0 - c * c)));
     }
-    double2* rr = tcs + G.ntheta + 1;
-    for (int i = threadIdx.x; i < G.nr; i += BLOCK) rr[i] = make_double2(G.rfr[i], G.rfr[i + 1]);
-    __syncthreads();
-    T.fr = fr; T.phsc = phsc; T.tcs = tcs; T.rr = rr;
-    return T;
+    double2* rr = (double2*)T.rr;
+    for (int i = tid; i <= G.nr; i += nt) rr[i] = make_double2(G.rfr[i], G.rfr[i < G.nr ? i + 1 : i]);
 }
+// The tables in LDS, staged by the block
+__device__ __forceinline__ TraceTabs stage_trace_tables(const DevGrid& G, double* lds) {
+    fill_trace_tables(G, lds, threadIdx.x, BLOCK);
+    __syncthreads();
+    return trace_tables_at(G, lds);
+}
+
+// The global copy of the GTAB kernels (one block, once per call before the engine loop): grids
+// whose tables exceed the 64 KiB k_trace stages in LDS (e.g. a fine P-T gas profile of ~2000
+// radial faces; the reference allocates any grid, ARTES.f90:2237-2307) read them from L2
+__global__ __launch_bounds__(BLOCK) void k_fill_trace_tables(DevGrid G) { fill_trace_tables(G, G.ttab, threadIdx.x, BLOCK); }
 
 // min of two doubles, one v_min_f64 without the canonicalising v_max the IEEE-mode fmin
 // needs on unknown operands.  A quiet-NaN operand (or_nan below: "no crossing") yields the
@@ -485,6 +507,34 @@ __device__ __forceinline__ double radial_tr(const TraceTabs& T, double b0, doubl
     return min_nonan(or_nan(vA, sA), or_nan(vB, sB));
 }
 
+// The radial family right after a sphere crossing, inside the radial-form step (the fused
+// step, k_trace): radial_tr for a packet on face (1, nfi) of its new shell `rr` -- on the
+// shell's inner sphere after an outward crossing (s_in = side), on its outer one after an
+// inward crossing (s_out = !side) -- with alt = false (a lane steps radially only with its
+// alt bit clear).  Within a monotone run of the trace the rules resolve the same way every
+// time: inwards the inner sphere's near root sA while the ray reaches it, outwards the outer
+// sphere's far root sB, and at the turn (the ray misses the inner sphere) the far root of the
+// sphere just crossed, at 1e-3 m (ARTES.f90:2885-3010).  The same operations in the same order
+// as radial_tr, so the same bits; only the two face tests are known from the step's side.
+// The 1e100 caps of radial_tr are left out: the roots and the trace parameter lie within 4 r_top
+// of the trace's start, and grids are limited to r_top < 1e40 m (artes_grid_create).
+// A NaN (no crossing: the other face next, `alt`) sends the lane back to radial_tr.
+__device__ __forceinline__ double radial_next(const double2 rr, double b0, double pm, double t, bool side, const TraceK& K,
+                                              bool& outer) {
+    const bool in_ok = (t < -b0) & (rr.x >= pm) & !side;
+    const bool ch = !in_ok;
+    const double r = ch ? rr.y : rr.x;
+    const double disc = (r - pm) * (r + pm);
+    const double sq = fast_sqrt_nan0(disc);
+    const double sA = -b0 - sq, sB = sq - b0;
+    const double dA = sA - t, dB = sB - t;
+    const double tmin = (ch & !side) ? K.tol_same : K.tol;
+    const bool ok = dA != dB;
+    const bool vA = ok & (dA > tmin), vB = ok & (dB > tmin);
+    outer = ch;
+    return min_nonan(or_nan(vA, sA), or_nan(vB, sB));
+}
+
 // ---------------------------------------------- phi family, trace-relative (TREL) ---
 // The half-plane through the z axis at phi_k meets the trace at s = num_k(p0) / den_k,
 // num = x sin phi_k - y cos phi_k, den = n_y cos phi_k - n_x sin phi_k (ARTES.f90:3292-3350):
@@ -545,11 +595,12 @@ __device__ __noinline__ void flow_segment(double* flow_g, double* flow_t, int ce
 //
 // FLOW instantiations add the energy-transport diagnostics to propagation segments.
 // NREP: steps per loop iteration (see the loop).
-template <bool G3D, bool OBL, int WPE, bool FLOW = false, int NREP = 8>
+// GTAB: the face tables in global memory (G.ttab, k_fill_trace_tables) instead of LDS.
+template <bool G3D, bool OBL, int WPE, bool FLOW = false, int NREP = 8, bool GTAB = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_trace(DevGrid G, DevRun R, Pool S, SubLists SL) {
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_tab[];
-    const TraceTabs T = stage_trace_tables(G, s_tab);
+    const TraceTabs T = GTAB ? trace_tables_at(G, G.ttab) : stage_trace_tables(G, s_tab);
     const int n = *L.trace_in_n;
     const int split = *L.trace_in_split;   // [0, split): new packets' traces; then k_event's, stored backwards
     const int home = sub_block() & 7;
@@ -1077,6 +1128,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             double best_abs, best;
             int w;
             bool fast, do_step;
+            bool rstep = false;   // (radial-form slots: the fused radial step)
+            double bestr = 0.0;
             if constexpr (TREL) {
                 // A. The radial family, whenever its entry is not exact (pending bit 0): the last
                 // step crossed a sphere (99.9 % of all crossings on the bench grid), a trace starts,
@@ -1096,6 +1149,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     dbg_r = retry; dbg_u = true;
 #endif
                 }
+                // A'. Radial-form slots: the lane steps onto its sphere when the radial entry is
+                // exact, the nearest one (ties to the radial family; NaN theta / phi entries are no
+                // candidates) and beyond 1e-9 m -- B's choice with w = 0 and a fast step (a radial
+                // entry is finite or NaN, never +inf).  B and C below run only when some lane of
+                // the wave does neither this nor A again but has a theta / phi bound pending.
+                if (!generic_slot) {
+                    bestr = e0 - tpar;
+                    rstep = !(pending & 1) & (bestr > K.step_min);
+                    if constexpr (G3D) rstep = rstep & !(e0 > min_nonan(e1, e2));
+                }
+                do_step = false;
+                best_abs = e0; best = bestr; w = 0; fast = rstep;
+                if (generic_slot || (G3D && __ballot(!rstep & (pending != 0) & !(pending & 1)))) {
                 // B. The choice: the nearest of the three entries.  A lane steps unless a pending
                 // family blocks it -- its bound is the nearest entry, or some family is pending and
                 // nothing lies beyond 1e-9 m -- (the reference's choice whenever it steps: a pending
@@ -1171,10 +1237,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     }
                     }   // any tp
                 }
-                TM_TICK(tev);
-                TM_ADD(2, tev - t_rep);
                 // D. The step below (a lane that evaluated theta / phi above steps in its next one)
                 do_step = !blocked;
+                }   // B, C
+                TM_TICK(tev);
+                TM_ADD(2, tev - t_rep);
             } else {
                 // ------------------------------------------- evaluate one face family
     #ifdef ARTES_NBF
@@ -1248,16 +1315,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             // that is not beyond 1e-9 m (ARTES.f90:3358-3418), next_cell (2671-2798), the
             // optical-depth sum and the trace ends (625-778, 848-941, 4739-4761)
 #ifdef ARTES_DEBUG_LANES
-            dbg_rstep += __popcll(__ballot(do_step));
-            dbg_rblock += __popcll(__ballot(!do_step));
+            dbg_rstep += __popcll(__ballot(generic_slot ? do_step : rstep));
+            dbg_rblock += __popcll(__ballot(!(generic_slot ? do_step : rstep)));
 #endif
-            if (do_step) {
-                if (!generic_slot) {
-                    if (w == 0 && fast) {
-                    // The radial form of the step (trace-relative kernels, see NSLOT): the generic
-                    // step below with w = 0 and a fast choice, the same results
-                    const int kn = tcr + ((sides & 1) ? 1 : -1);
+            if (!generic_slot) {
+                if (rstep) {
+                    // The fused radial step (trace-relative kernels, see NSLOT): the generic step
+                    // below with w = 0 and a fast choice, the same results, and then at once the
+                    // radial family of the new shell (radial_next: radial_tr's result for the packet
+                    // on the sphere it just crossed), so the lane's next slot needs no evaluation.
+                    // The new shell's radii are read before the trace-end tests (rr[kn] for
+                    // kn = -1 .. nr: padded, used only when the packet stays in the grid).
                     const bool side = sides & 1;
+                    const int kn = tcr + (side ? 1 : -1);
+                    const double2 rrn = T.rr[kn];
                     const int nfi = side ? kn : tcr;
                     const bool runaway = ncross >= nlim;
                     const bool exit = side & (nfi == G.nr) & !runaway;
@@ -1270,7 +1341,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     }
     #endif
                     ncross++;
-                    const double tau_cell = best * k;
+                    const double tau_cell = bestr * k;
                     const bool prop = (mode == S_PROP);
                     const bool hit = prop && tacc + tau_cell > ttgt;
                     const bool stop = err || exit || surf || hit;
@@ -1280,20 +1351,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     const bool hitpark = prop & hit & !err;
                     if (!hitpark) {
                         tacc += tau_cell;
-                        tpar = best_abs;
+                        tpar = e0;
                         tft = 1; tfi = nfi;
                     }
                     if (!stop) {
                         cell += kn - tcr;
                         tcr = kn;
                         load_cell();
-                        pending |= 1;
+                        bool outer;
+                        const double dm = radial_next(rrn, b0, pm, tpar, side, K, outer);
+                        e0 = dm;
+                        sides = (sides & ~1) | (outer ? 1 : 0);
+                        pending |= (dm < K.inf) ? 0 : 1;   // (NaN: radial_tr in the next slot, alt)
                     } else {
                         parked = hitpark ? 4 : (PK_END | (exit ? PK_EXIT : 0) | (surf ? PK_SURF : 0) | (runaway ? PK_ERR31 | PK_RUNAWAY : 0) |
                                                 (err ? PK_ERR : 0));
                     }
-                    }   // w == 0 && fast
-                } else {
+                }   // rstep
+            } else if (do_step) {
+                {
                     if (!fast) {   // rare (every family exact here)
                         const double r0 = TREL ? e0 - tpar : e0, r1 = TREL ? e1 - tpar : e1, r2 = TREL ? e2 - tpar : e2;
                         const double t0 = or_nan(r0 > 1.e-9, r0);

@@ -87,6 +87,29 @@ __global__ void reduce_detector(const double* __restrict__ copies, size_t stride
     }
 }
 
+// det_ordered (kernel_event.hpp, fix_add): the nfix fixed-point copies of planes 0-9 summed in
+// 128-bit integers (exact, so in any order) and converted once, into copy 0 of the floating-point
+// detector (whose planes 0-9 nothing else writes then): reduce_detector then adds zeros to it
+__global__ void reduce_fixed(const unsigned long long* __restrict__ fix, size_t fix_stride, int nfix, size_t plane,
+                             double* __restrict__ copy0) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 10 * plane) return;
+    unsigned long long lo = 0, hi = 0;
+    for (int c = 0; c < nfix; c++) {
+        const unsigned long long l = fix[(size_t)c * fix_stride + 2 * i], h = fix[(size_t)c * fix_stride + 2 * i + 1];
+        const unsigned long long s = lo + l;
+        hi += h + (s < lo ? 1ull : 0ull);
+        lo = s;
+    }
+    const bool neg = (long long)hi < 0;
+    if (neg) {
+        hi = ~hi + (lo == 0 ? 1ull : 0ull);
+        lo = 0ull - lo;
+    }
+    const double v = (double)hi * 0x1p-16 + (double)lo * 0x1p-80;
+    copy0[i] = neg ? -v : v;
+}
+
 }  // namespace artes
 
 // ================================================================= C ABI ===
@@ -103,7 +126,7 @@ using namespace artes;
 enum TuneKey : int {
     T_ENGINE, T_POOL, T_STEPS, T_REFILL, T_STATIC, T_DGRAB, T_BATCH, T_BATCH_MIN, T_HBATCH, T_GBATCH, T_DEFER,
     T_BACKWARD, T_EMIT_FIRST, T_LATE_APPEND, T_PIX1, T_DET_LDS, T_EVENT_LDS, T_EVENT_LDSC, T_EVENT_BLOCK, T_EVENT_BPC,
-    T_TRACE_BPC, T_WPE, T_MSYM, T_MAX_IT, T_VERBOSE, T_NUM
+    T_TRACE_BPC, T_WPE, T_MSYM, T_MAX_IT, T_VERBOSE, T_TRACE_GTAB, T_DET_ORDERED, T_NUM
 };
 struct TuneSpec {
     const char* name;
@@ -135,6 +158,8 @@ static const TuneSpec TUNE[T_NUM] = {
     {"msym", 0, 1},              // block-diagonal matrices read as 4 elements per row
     {"max_it", 1, 1LL << 40},    // engine iterations before a call fails
     {"verbose", 0, 1},           // one stderr line per call (pool, iterations, kernel choice)
+    {"trace_gtab", 0, 1},        // k_trace's face tables in global memory (automatic beyond 64 KiB)
+    {"det_ordered", 0, 1},       // detector partials summed in a fixed order: bit-reproducible images
 };
 
 struct artes_grid {
@@ -162,6 +187,10 @@ struct artes_grid {
     double* d_rec = nullptr;
     size_t rec_cap = 0;
     double* d_flow = nullptr;         // scratch flow accumulators of the host-pointer variant [7][ncell]
+    double* d_ttab = nullptr;         // k_trace's face tables in global memory (GTAB kernels)
+    size_t ttab_cap = 0;
+    unsigned long long* d_fix = nullptr;   // det_ordered: fixed-point detector copies
+    size_t fix_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     int max_blocks = 0;
@@ -181,6 +210,7 @@ struct artes_grid {
     int trace_blocks = 0;
     int trace_nrep = 0;                   // steps per iteration of the last k_trace launched
     std::string last_trace, last_event;   // the kernel instantiations of the last call (artes_last_launch)
+    int last_engine = 0;                  // the last call's engine: 0 none launched, 1 event, 2 persistent
     std::string launch_info;
     long long last_iterations = 0;
     // occupancy answers per (kernel, dynamic LDS bytes), queried once per grid
@@ -324,11 +354,11 @@ void artes_grid_destroy(artes_grid* g) {
     void* ptrs[] = {g->d_rf2, g->d_thetaf, g->d_tan2, g->d_phif, g->d_phis, g->d_phic, g->d_kappa, g->d_albedo, g->d_ka,
                     g->d_mats, g->d_cums, g->d_sc2, g->d_ss2, g->d_tplane, g->d_matid, g->d_copies, g->d_out,
                     g->d_tot, g->d_cnt, g->d_cnt_part, g->d_tot_part, g->d_err, g->d_rec, g->d_rfront, g->d_tcos, g->d_th_cdf, g->d_th_weight,
-                    g->d_flow};
+                    g->d_flow, g->d_ttab};
     for (void* p : ptrs)
         if (p) hipFree(p);
     void* eptrs[] = {g->pool_mem, g->d_lists[0], g->d_lists[1], g->d_event, g->d_emit, g->d_counts, g->d_grab, g->d_next,
-                     g->d_owner};
+                     g->d_owner, g->d_fix};
     for (void* p : eptrs)
         if (p) hipFree(p);
     for (auto& W : g->wl) {
@@ -355,6 +385,9 @@ int32_t artes_grid_create(const artes_grid_desc* desc, int32_t device, artes_gri
     } catch (const std::exception& e) {
         return fail(-22, e.what());
     }
+    // (k_trace's fused radial step leaves out the 1e100 caps of the radial roots, which no
+    // grid below 1e40 m can reach: kernel_trace.hpp, radial_next)
+    if (!(g->T.rfront[g->T.nr] < 1.e40)) return fail(-22, "radial grid beyond 1e40 m");
     HIP_TRY(hipSetDevice(device));
     const HostTables& T = g->T;
     HIP_TRY(upload(&g->d_rf2, T.rf2));
@@ -485,11 +518,14 @@ static int32_t ensure_pool(artes_grid* g, uint64_t n) {
     // record accesses of k_event and k_emit missed in the TLBs past ~30 M slots; split
     // over the XCDs (NSUB sub-engines) they no longer do up to 50 M (pool sweep in
     // DESIGN.md §3)
-    long long P = tv(g, T_POOL, (long long)g->num_cus * 131072);
-    P = std::max<long long>(1024, std::min<long long>(P, 1LL << 26));
-    P = std::min<long long>(P, std::max<long long>((long long)std::min<uint64_t>(n, 1ULL << 26), 1024));
-    P = (P + 64 * NSUB - 1) / (64 * NSUB) * (64 * NSUB);   // NSUB sub-engines of whole waves of slots
-    if (g->pool_mem && g->pool.P >= P) return 0;
+    long long Pmax = tv(g, T_POOL, (long long)g->num_cus * 131072);
+    Pmax = std::max<long long>(1024, std::min<long long>(Pmax, 1LL << 26));
+    long long P = std::min<long long>(Pmax, std::max<long long>((long long)std::min<uint64_t>(n, 1ULL << 26), 1024));
+    auto whole = [](long long v) { return (v + 64 * NSUB - 1) / (64 * NSUB) * (64 * NSUB); };   // NSUB sub-engines of whole waves of slots
+    P = whole(P);
+    // a pool at least this call's size is kept unless it exceeds the pool setting (the "pool"
+    // key set below an earlier call's pool reallocates: every key overrides the schedule)
+    if (g->pool_mem && g->pool.P >= P && g->pool.P <= whole(Pmax)) return 0;
     free_pool(g);
     HIP_TRY(hipMalloc(&g->pool_mem, (size_t)P * (sizeof(Slot) + sizeof(SlotDiag))));
     g->pool.P = (int)P;
@@ -525,42 +561,50 @@ static int round_sub(int blocks) { return std::max(NSUB, (blocks + NSUB - 1) / N
 #ifndef ARTES_COARSE_NREP
 #define ARTES_COARSE_NREP 4
 #endif
-template <bool G3D, bool OBL, int WPE, bool FLOW = false, int NREP = 8>
+template <bool G3D, bool OBL, int WPE, bool FLOW = false, int NREP = 8, bool GTAB = false>
 static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L, hipStream_t stream) {
-    const size_t lds = trace_table_bytes(G.nr, G.ntheta, G.nphi);
-    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW, NREP>, lds);
+    const size_t lds = GTAB ? 0 : trace_table_bytes(G.nr, G.ntheta, G.nphi);
+    const int per_cu = bpc > 0 ? bpc : blocks_per_cu(g, k_trace<G3D, OBL, WPE, FLOW, NREP, GTAB>, lds);
     g->trace_blocks = round_sub(per_cu * g->num_cus);
     g->trace_nrep = NREP;
     if (g->last_trace.empty()) {
         char b[80];
-        snprintf(b, sizeof(b), "k_trace<%d,%d,%d,%d,%d>", (int)G3D, (int)OBL, WPE, (int)FLOW, NREP);
+        if (GTAB) snprintf(b, sizeof(b), "k_trace<%d,%d,%d,%d,%d,1>", (int)G3D, (int)OBL, WPE, (int)FLOW, NREP);
+        else snprintf(b, sizeof(b), "k_trace<%d,%d,%d,%d,%d>", (int)G3D, (int)OBL, WPE, (int)FLOW, NREP);
         g->last_trace = b;
     }
     timed(g, ARTES_K_TRACE, stream, [&] {
-        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW, NREP>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
+        hipLaunchKernelGGL((k_trace<G3D, OBL, WPE, FLOW, NREP, GTAB>), dim3(g->trace_blocks), dim3(BLOCK), lds, stream, G, R, g->pool, L);
     });
 }
 
 // k_trace variant: 3D or radial-only grid, spheroidal (oblate) or spherical planet,
-// occupancy target (waves per SIMD the register budget is sized for)
+// occupancy target (waves per SIMD the register budget is sized for), face tables in LDS or
+// in global memory (GTAB)
 // (steps: k_trace's steps per loop iteration, 8 or 4; see trace_steps)
-template <bool G3D>
-static void launch_trace_any(artes_grid* g, int wpe, int steps, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L,
+template <bool G3D, bool GTAB>
+static void launch_trace_tab(artes_grid* g, int wpe, int steps, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L,
                              hipStream_t stream) {
     const bool oblate = !(G.ax2 == 1.0 && G.by2 == 1.0 && G.cz2 == 1.0 && G.a == 1.0 && G.b == 1.0);
     if (R.flow_g || R.flow_t) {   // diagnostics: one occupancy target only
-        if (oblate) launch_trace<G3D, true, 4, true>(g, bpc, G, R, L, stream);
-        else launch_trace<G3D, false, 4, true>(g, bpc, G, R, L, stream);
+        if (oblate) launch_trace<G3D, true, 4, true, 8, GTAB>(g, bpc, G, R, L, stream);
+        else launch_trace<G3D, false, 4, true, 8, GTAB>(g, bpc, G, R, L, stream);
     } else if (oblate) {
-        if (wpe == 3) launch_trace<G3D, true, 3>(g, bpc, G, R, L, stream);
-        else launch_trace<G3D, true, 4>(g, bpc, G, R, L, stream);
+        if (wpe == 3) launch_trace<G3D, true, 3, false, 8, GTAB>(g, bpc, G, R, L, stream);
+        else launch_trace<G3D, true, 4, false, 8, GTAB>(g, bpc, G, R, L, stream);
     } else if (wpe == 3) {
-        launch_trace<G3D, false, 3>(g, bpc, G, R, L, stream);
+        launch_trace<G3D, false, 3, false, 8, GTAB>(g, bpc, G, R, L, stream);
     } else if (G3D && steps == 4) {
-        launch_trace<G3D, false, 4, false, ARTES_COARSE_NREP>(g, bpc, G, R, L, stream);
+        launch_trace<G3D, false, 4, false, ARTES_COARSE_NREP, GTAB>(g, bpc, G, R, L, stream);
     } else {
-        launch_trace<G3D, false, 4>(g, bpc, G, R, L, stream);
+        launch_trace<G3D, false, 4, false, 8, GTAB>(g, bpc, G, R, L, stream);
     }
+}
+template <bool G3D>
+static void launch_trace_any(artes_grid* g, bool gtab, int wpe, int steps, int bpc, const DevGrid& G, const DevRun& R,
+                             const SubLists& L, hipStream_t stream) {
+    if (gtab) launch_trace_tab<G3D, true>(g, wpe, steps, bpc, G, R, L, stream);
+    else launch_trace_tab<G3D, false>(g, wpe, steps, bpc, G, R, L, stream);
 }
 
 // diagnostics (ARTES_VERBOSE) when the engine does not terminate: the transport state of
@@ -614,7 +658,23 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     // more lanes idle for the rest of an iteration (profiles/r04/ab/trace_nrep*_ab.txt);
     // tuning "steps" = 4 | 8 overrides (3D grids; the oblate, flow and wpe = 3 kernels have 8)
     const int trace_steps = (int)tv(g, T_STEPS, G.ncell < 4096 ? 4 : 8);
-    if (trace_table_bytes(G.nr, G.ntheta, G.nphi) > 65536) return fail(-22, "face tables exceed the 64 KiB LDS budget of k_trace");
+    // k_trace's face tables: in LDS up to 64 KiB (two blocks per CU at most then), beyond that
+    // in global memory (GTAB kernels, L2-resident: ~2000 radial faces and more); tuning
+    // "trace_gtab" = 1 forces the global tables (tests)
+    const size_t ttab_bytes = trace_table_bytes(G.nr, G.ntheta, G.nphi);
+    const bool gtab = ttab_bytes > 65536 || tv(g, T_TRACE_GTAB, 0) != 0;
+    DevGrid GT = G;
+    if (gtab) {
+        if (g->ttab_cap < ttab_bytes) {
+            if (g->d_ttab) hipFree(g->d_ttab);
+            g->d_ttab = nullptr;
+            g->ttab_cap = 0;
+            HIP_TRY(hipMalloc((void**)&g->d_ttab, ttab_bytes));
+            g->ttab_cap = ttab_bytes;
+        }
+        GT.ttab = g->d_ttab;
+        hipLaunchKernelGGL(k_fill_trace_tables, dim3(1), dim3(BLOCK), 0, stream, GT);
+    }
     // scattering tables in LDS for k_event when they fit next to one another (a few
     // distinct matrices: uniform and layered atmospheres); otherwise read from L2
     const size_t ev_bytes = event_table_doubles(G.nmat, G.msym != 0) * sizeof(double);
@@ -722,13 +782,22 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     else if (ev_lds) ev_v = 10;
     else if (det_lds && ev_block == EVB) ev_v = 11;
     else if (det_lds) ev_v = 12;
-    static const struct { int lt, ld, p1, big, lc; } EVV[14] = {
+    // det_ordered: the fixed-point detector (k_event ORD), EVB-thread blocks, the tables in LDS as
+    // far as they fit alone
+    if (R.fix) {
+        ev_v = ev_lds ? 14 : (cum_bytes <= lds_cap && tv(g, T_EVENT_LDSC, 1) != 0) ? 15 : 16;
+        ev_blocks = round_sub((ev_v == 14 ? blocks_per_cu(g, k_event<true, false, false, EVB, false, true>, ev_bytes, EVB)
+                               : ev_v == 15 ? blocks_per_cu(g, k_event<false, false, false, EVB, true, true>, cum_bytes, EVB)
+                                            : blocks_per_cu(g, k_event<false, false, false, EVB, false, true>, 0, EVB)) * g->num_cus);
+    }
+    static const struct { int lt, ld, p1, big, lc; } EVV[17] = {
         {0, 0, 0, 0, 0}, {1, 0, 1, 1, 0}, {0, 0, 1, 1, 1}, {0, 1, 0, 1, 1}, {0, 0, 0, 1, 1}, {0, 0, 1, 1, 0}, {1, 0, 1, 0, 0},
-        {0, 0, 1, 0, 0}, {1, 1, 0, 1, 0}, {1, 1, 0, 0, 0}, {1, 0, 0, 0, 0}, {0, 1, 0, 1, 0}, {0, 1, 0, 0, 0}, {0, 0, 0, 0, 0}};
+        {0, 0, 1, 0, 0}, {1, 1, 0, 1, 0}, {1, 1, 0, 0, 0}, {1, 0, 0, 0, 0}, {0, 1, 0, 1, 0}, {0, 1, 0, 0, 0}, {0, 0, 0, 0, 0},
+        {1, 0, 0, 1, 0}, {0, 0, 0, 1, 1}, {0, 0, 0, 1, 0}};
     {
         char b[96];
-        snprintf(b, sizeof(b), "k_event<%d,%d,%d,%d,%d>", EVV[ev_v].lt, EVV[ev_v].ld, EVV[ev_v].p1, EVV[ev_v].big ? EVB : BLOCK,
-                 EVV[ev_v].lc);
+        snprintf(b, sizeof(b), ev_v >= 14 ? "k_event<%d,%d,%d,%d,%d,1>" : "k_event<%d,%d,%d,%d,%d>", EVV[ev_v].lt, EVV[ev_v].ld,
+                 EVV[ev_v].p1, EVV[ev_v].big ? EVB : BLOCK, EVV[ev_v].lc);
         g->last_event = b;
     }
     auto launch_event = [&](const SubLists& L) {
@@ -745,6 +814,9 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         case 10: hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L); break;
         case 11: hipLaunchKernelGGL((k_event<false, true, false, EVB>), dim3(ev_blocks), dim3(EVB), det_bytes, stream, G, R, g->pool, L); break;
         case 12: hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L); break;
+        case 14: hipLaunchKernelGGL((k_event<true, false, false, EVB, false, true>), dim3(ev_blocks), dim3(EVB), ev_bytes, stream, G, R, g->pool, L); break;
+        case 15: hipLaunchKernelGGL((k_event<false, false, false, EVB, true, true>), dim3(ev_blocks), dim3(EVB), cum_bytes, stream, G, R, g->pool, L); break;
+        case 16: hipLaunchKernelGGL((k_event<false, false, false, EVB, false, true>), dim3(ev_blocks), dim3(EVB), 0, stream, G, R, g->pool, L); break;
         default: hipLaunchKernelGGL((k_event<false, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L); break;
         }
     };
@@ -754,7 +826,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     const long long max_it = tv(g, T_MAX_IT, 2000000LL);
     for (;;) {
         SubLists L = lists(in);
-        launch_trace_any<G3D>(g, wpe, trace_steps, trace_bpc, G, R, L, stream);
+        launch_trace_any<G3D>(g, gtab, wpe, trace_steps, trace_bpc, GT, R, L, stream);
         timed(g, ARTES_K_EVENT, stream, [&] { launch_event(L); });
         timed(g, ARTES_K_EMIT, stream, [&] { launch_emit(L); });
         timed(g, ARTES_K_AUX, stream, [&] {
@@ -797,6 +869,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     if (!p) return fail(-22, "null params");
     g->last_trace.clear();
     g->last_event.clear();
+    g->last_engine = 0;
     if (p->photon_source != 1 && p->photon_source != 2) return fail(-22, "photon_source must be 1 (star) or 2 (planet)");
     if (!use_event_engine(g) && (p->photon_source != 1 || p->surface_albedo > 0.0 || flow_g || flow_t))
         return fail(-38, "the persistent engine supports the star source without surface reflection or flow output only");
@@ -813,11 +886,29 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
         g->copies_cap = stride * ncopy;
     }
     HIP_TRY(hipMemsetAsync(g->d_copies, 0, stride * ncopy * sizeof(double), stream));
+    // det_ordered: the fixed-point copies of planes 0-9, one per CU (a k_event block's copy is its
+    // index modulo nfix) within 256 MiB
+    const bool det_ordered = tv(g, T_DET_ORDERED, 0) != 0;
+    if (det_ordered && !use_event_engine(g)) return fail(-38, "det_ordered: the event engine only");
+    const size_t fix_stride = 20 * plane;
+    int nfix = 0;
+    if (det_ordered) {
+        nfix = (int)std::max<size_t>(1, std::min<size_t>((size_t)g->num_cus, ((size_t)256 << 20) / (fix_stride * 8)));
+        if (g->fix_cap < fix_stride * nfix) {
+            if (g->d_fix) hipFree(g->d_fix);
+            g->d_fix = nullptr;
+            g->fix_cap = 0;
+            HIP_TRY(hipMalloc((void**)&g->d_fix, fix_stride * nfix * sizeof(unsigned long long)));
+            g->fix_cap = fix_stride * nfix;
+        }
+        HIP_TRY(hipMemsetAsync(g->d_fix, 0, fix_stride * nfix * sizeof(unsigned long long), stream));
+    }
 
     DevGrid G;
     G.nr = T.nr; G.ntheta = T.ntheta; G.nphi = T.nphi; G.ncell = T.ncell; G.nmat = T.nmat;
     G.cell_depth = p->cell_depth >= 0 ? p->cell_depth : T.cell_depth[p->wl_index];
     G.rfr = g->d_rfront; G.tcos = g->d_tcos;
+    G.ttab = nullptr;
     G.ox = T.oblate_x; G.oy = T.oblate_y; G.oz = T.oblate_z;
     G.th_cdf = nullptr; G.th_weight = nullptr; G.th_ncdf = 0; G.th_cd0 = 0; G.th_total = 0.0;
     if (p->photon_source == 2) {   // thermal tables of this wavelength (ARTES.f90:2359-2453)
@@ -946,6 +1037,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     R.x_max = p->x_max; R.y_max = p->y_max; R.fstop = p->fstop; R.pmin = p->photon_minimum;
     R.surface_albedo = p->surface_albedo; R.theta_star = p->theta_star; R.phi_star = p->phi_star;
     R.det = g->d_copies; R.det_stride = stride; R.ncopy = ncopy;
+    R.fix = det_ordered ? g->d_fix : nullptr; R.fix_stride = fix_stride; R.nfix = std::max(nfix, 1);
     R.tot2 = g->d_tot_part; R.cnt = g->d_cnt_part; R.err = err_out; R.rec = rec;
     HIP_TRY(hipMemsetAsync(g->d_cnt_part, 0, CNT_COPIES * CNT_STRIDE * sizeof(unsigned long long), stream));
     HIP_TRY(hipMemsetAsync(g->d_tot_part, 0, CNT_COPIES * CNT_STRIDE * sizeof(double), stream));
@@ -958,6 +1050,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
             return fail(-22, "event engine packs cells into 12/10/10 bits: nr < 4096, ntheta < 1024, nphi < 1024");
         if ((long long)T.ncell >= (1LL << 28))
             return fail(-22, "event engine addresses the per-cell table with 32-bit byte offsets: ncell < 2^28");
+        g->last_engine = 1;
         int32_t rc = g3d ? run_event_engine<true>(g, G, R, rec != nullptr, stream)
                          : run_event_engine<false>(g, G, R, rec != nullptr, stream);
         if (rc) {
@@ -970,6 +1063,7 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     } else if (n > 0) {
         uint64_t want = (n + BLOCK - 1) / BLOCK;
         int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)g->max_blocks));
+        g->last_engine = 2;
         timed(g, ARTES_K_PERSISTENT, stream, [&] {
             if (rec) {
                 if (g3d) hipLaunchKernelGGL((transport_kernel<true, true>), dim3(blocks), dim3(BLOCK), 0, stream, G, R);
@@ -985,6 +1079,9 @@ static int32_t launch(artes_grid* g, const artes_run_params* p, uint64_t first, 
     g->timed = true;
     const int rb = (int)((16 * plane + 255) / 256);
     timed(g, ARTES_K_AUX, stream, [&] {
+        if (det_ordered)
+            hipLaunchKernelGGL(reduce_fixed, dim3((unsigned)((10 * plane + 255) / 256)), dim3(256), 0, stream,
+                               (const unsigned long long*)g->d_fix, fix_stride, nfix, plane, g->d_copies);
         hipLaunchKernelGGL(reduce_detector, dim3(rb), dim3(256), 0, stream, (const double*)g->d_copies, stride, ncopy, plane, det_out);
         hipLaunchKernelGGL(sum_counters, dim3(1), dim3(64), 0, stream, (const unsigned long long*)g->d_cnt_part, cnt_out,
                            (const double*)g->d_tot_part, tot_out);
@@ -1122,7 +1219,11 @@ int32_t artes_run_trace(artes_grid* g, const artes_run_params* p, uint64_t first
 
 const char* artes_last_launch(artes_grid* g) {
     if (!g) return "";
-    g->launch_info = g->last_trace.empty() ? std::string("persistent") : g->last_trace + " " + g->last_event;
+    // (recorded by launch(): "none" for an n = 0 call, or an event-engine call that failed before
+    // its first k_trace launch)
+    if (g->last_engine == 2) g->launch_info = "persistent";
+    else if (g->last_engine == 1 && !g->last_trace.empty()) g->launch_info = g->last_trace + " " + g->last_event;
+    else g->launch_info = "none";
     return g->launch_info.c_str();
 }
 

@@ -84,15 +84,32 @@ def shard(n_packets: int, rank: int, world: int) -> tuple[int, int]:
 
 def group_active() -> bool:
     """A process group is open (``init`` with several ranks, or one rank under
-    ARTES_DIST_FORCE=1): the reductions then go through it even at world size 1, so a
-    one-rank run exercises the collective path.  (No torch import when none was made.)"""
+    ARTES_DIST_FORCE=1).  (No torch import when none was made.)"""
     d = sys.modules.get("torch.distributed")
     return d is not None and d.is_available() and d.is_initialized()
 
 
+def reduces(world: int) -> bool:
+    """Whether a call made for ``world`` ranks sums over the open process group: only when the
+    group has exactly that many ranks.  A one-rank group (ARTES_DIST_FORCE=1) exercises the
+    collective path at world size 1; a caller's unsharded run (world 1) inside a host
+    application's own multi-rank group is not reduced, since every rank of that group then
+    transported every packet.  A sharded call (world > 1) without a matching group fails."""
+    if not group_active():
+        if world > 1:
+            raise RuntimeError(f"a {world}-rank call needs an open process group (artes_amd.dist.init)")
+        return False
+    import torch.distributed as dist
+
+    size = dist.get_world_size()
+    if world > 1 and size != world:
+        raise RuntimeError(f"a {world}-rank call inside a process group of {size} ranks")
+    return size == max(world, 1)
+
+
 def allreduce_numpy(arrays: list[np.ndarray], world: int) -> list[np.ndarray]:
     """Sum host arrays over ranks: in place under gloo, through the rank's GPU under nccl."""
-    if world <= 1 and not group_active():
+    if not reduces(world):
         return arrays
     import torch
     import torch.distributed as dist
@@ -119,7 +136,7 @@ def broadcast_int(value: int, r: Rank) -> int:
     """Rank 0's non-negative ``value`` (< 2^64) on every rank: the clock seed of a CLI run
     must be the same on every shard, or the global packet ids would not map to one RNG
     stream set (the result would then depend on the rank start times)."""
-    if r.world <= 1 and not group_active():
+    if not reduces(r.world):
         return int(value)
     parts = np.array([value >> 32, value & 0xFFFFFFFF], dtype=np.float64) if r.rank == 0 else np.zeros(2)
     (out,) = allreduce_numpy([parts], r.world)   # exact: each half < 2^32
@@ -131,7 +148,7 @@ def run_sharded(transport, n_packets: int, seed: int, r: Rank):
     the results over all ranks (host tensors; the GPU bench uses device tensors + RCCL)."""
     first, count = shard(n_packets, r.rank, r.world)
     res = transport(first, count, seed)
-    if r.world > 1 or group_active():
+    if reduces(r.world):
         flows = [k for k in ("flow_global", "flow_latitudinal") if getattr(res, k, None) is not None]
         red = allreduce_numpy([res.det, res.totals, res.counters.astype(np.float64), res.err.astype(np.float64)]
                               + [getattr(res, k) for k in flows], r.world)

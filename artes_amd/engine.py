@@ -16,6 +16,10 @@ from .abi import (ARTES_ABI_VERSION, ARTES_NUM_COUNTERS, ARTES_NUM_ERR, ARTES_NU
                   GridArrays, GridDesc, RunParams)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# ARTES_LIB_PATH selects another build of the engine (the A/B tools); a development build
+# (ARTES_DEV_KNOBS: its schedule also follows ARTES_* environment variables) loads only with the
+# explicit opt-in ARTES_DEV_LIB=1, so a stray path cannot bring environment-driven engine
+# selection back into a production run
 LIB_PATH = os.environ.get("ARTES_LIB_PATH") or os.path.join(HERE, "lib", "libartes_hip.so")
 
 _lib = None
@@ -25,7 +29,7 @@ KERNEL_NAMES = ("trace", "event", "emit", "aux", "persistent")   # ARTES_K_* ord
 # artes_set_tuning keys (include/artes_amd.h; transport.hip, TUNE)
 TUNING_KEYS = ("engine", "pool", "steps", "refill", "static", "dgrab", "batch", "batch_min", "hbatch", "gbatch", "defer",
                "backward", "emit_first", "late_append", "pix1", "det_lds", "event_lds", "event_ldsc", "event_block",
-               "event_bpc", "trace_bpc", "wpe", "msym", "max_it", "verbose")
+               "event_bpc", "trace_bpc", "wpe", "msym", "max_it", "verbose", "trace_gtab", "det_ordered")
 
 
 class EngineUnavailable(RuntimeError):
@@ -98,8 +102,16 @@ def lib():
     L.artes_last_launch.argtypes = [C.c_void_p]
     if L.artes_abi_version() != ARTES_ABI_VERSION:
         raise EngineUnavailable("ABI version mismatch")
+    if b"development build" in L.artes_build_info() and os.environ.get("ARTES_DEV_LIB") != "1":
+        raise EngineUnavailable(f"{LIB_PATH} is a development build (tuning from the environment): "
+                                "set ARTES_DEV_LIB=1 to load it deliberately")
     _lib = L
     return L
+
+
+def build_info() -> str:
+    """The loaded library's build string (``artes_build_info``)."""
+    return lib().artes_build_info().decode()
 
 
 def device_count() -> int:

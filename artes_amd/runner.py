@@ -39,10 +39,12 @@ from .config import PI, ConfigError, RunConfig, read_artes_in, split_key_value
 class Transport:
     """Packet-loop backend: the HIP engine on this rank's GPU."""
 
-    def __init__(self, atm: dict, device: int, oblateness: float):
+    def __init__(self, atm: dict, device: int, oblateness: float, tuning: dict | None = None):
         from .engine import Grid
 
         self.grid = Grid(atm, device=device, oblateness=oblateness)
+        if tuning:   # engine:<key>=<value> keys (RunConfig.engine)
+            self.grid.set_tuning(**tuning)
 
     def cell_depth(self, wl: int) -> int:
         return self.grid.cell_depth(wl)
@@ -136,7 +138,8 @@ def run(argv: list[str], root: str | None = None, transport_factory=None, stdout
         seed = dist.broadcast_int(int(time.time() * 1e6) & 0x7FFFFFFFFFFFFFFF, r)
     device = dist.device_of(r)
     if transport_factory is None:
-        transport = Transport(atm, device=device, oblateness=cfg.oblateness)
+        transport = (Transport(atm, device=device, oblateness=cfg.oblateness, tuning=cfg.engine) if cfg.engine
+                     else Transport(atm, device=device, oblateness=cfg.oblateness))
     else:
         transport = transport_factory(atm, device, cfg.oblateness)
     if r.rank == 0:

@@ -243,10 +243,14 @@ int32_t artes_run_trace(artes_grid* grid, const artes_run_params* params,
 /* Schedule tuning of one grid handle (development A/B runs and tests).  `key` names one
  * launch-schedule setting; `value` >= 0 overrides it, -1 restores the default (the measured
  * optimum).  No key except "engine" changes a per-packet result: they move the schedule only.
- * Keys: engine (0 event engine, 1 the fused persistent engine), pool (slots), steps (k_trace
+ * Keys: engine (0 event engine, 1 the fused persistent engine), pool (slots; a pool larger than
+ * the setting is reallocated at the next call), steps (k_trace
  * steps per iteration, 4 or 8, 3D grids), refill, static, dgrab, batch, batch_min, hbatch,
  * gbatch, defer, backward, emit_first, late_append, pix1, det_lds, event_lds, event_ldsc,
- * event_block (256 or 768), event_bpc, trace_bpc, wpe (3 or 4), msym, max_it, verbose
+ * event_block (256 or 768), event_bpc, trace_bpc, wpe (3 or 4), msym, max_it, verbose,
+ * trace_gtab (k_trace's face tables in global memory; automatic when they exceed 64 KiB),
+ * det_ordered (1: detector planes 0-11 summed as 128-bit fixed-point integers, so identical
+ * calls give identical bits; the packet-level moments stay floating-point sums)
  * (transport.hip, TUNE).  Returns -22 for an unknown key or a value outside the key's range.
  * The production library reads no environment variable: the reference's drop-in never sees
  * a schedule it did not ask for.  The development build (libartes_hip_dev.so) also takes
@@ -258,7 +262,8 @@ int64_t artes_get_tuning(const artes_grid* grid, const char* key);
 /* The kernel instantiations the last call on this grid launched, e.g.
  * "k_trace<1,0,4,0,8> k_event<1,1,0,768,0>" (template arguments of kernel_trace.hpp /
  * kernel_event.hpp: G3D, OBL, WPE, FLOW, NREP and LDS_T, LDS_D, PIX1, block, LDS_C), or
- * "persistent"; storage owned by the grid, valid until its next call. */
+ * "persistent", or "none" when the call launched no transport kernel (n = 0, or a failure
+ * before the first launch); storage owned by the grid, valid until its next call. */
 const char* artes_last_launch(artes_grid* grid);
 
 /* Last error message of the calling thread (static storage). */

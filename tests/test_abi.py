@@ -4,6 +4,8 @@ declared in include/artes_amd.h (no compute calls: this runs without a GPU)."""
 import ctypes
 import os
 import re
+import subprocess
+import sys
 
 import pytest
 
@@ -103,6 +105,25 @@ def test_production_library_reads_no_environment():
         assert "getenv" in _undefined_symbols(dev)
     lib = engine.lib()
     assert b"development build" not in lib.artes_build_info()
+
+
+def test_development_build_needs_opt_in(tmp_path):
+    """A development build named by ARTES_LIB_PATH does not load without ARTES_DEV_LIB=1 (its
+    schedule follows ARTES_* variables), and loads with it."""
+    dev = os.path.join(ROOT, "artes_amd", "lib", "libartes_hip_dev.so")
+    if not os.path.exists(dev):
+        pytest.skip("development build not built")
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from artes_amd import engine\n"
+            "try:\n    engine.lib(); print('loaded', engine.build_info())\n"
+            "except engine.EngineUnavailable as e:\n    print('refused', e)\n") % ROOT
+    env = {k: v for k, v in os.environ.items() if k != "ARTES_DEV_LIB"}
+    env["ARTES_LIB_PATH"] = dev
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert out.stdout.startswith("refused"), out.stdout + out.stderr
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         env=dict(env, ARTES_DEV_LIB="1"), timeout=300)
+    assert out.stdout.startswith("loaded") and "development build" in out.stdout, out.stdout + out.stderr
 
 
 def test_tuning_keys_without_device():

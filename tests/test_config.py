@@ -41,6 +41,21 @@ def test_clamps_and_order_dependence():
 def test_unknown_key_is_fatal():
     with pytest.raises(ConfigError, match="Wrong keyword"):
         RunConfig().apply("detector:foo", "1")
+    with pytest.raises(ConfigError, match="Wrong keyword"):
+        RunConfig().apply("engine:nonsense", "1")
+
+
+def test_engine_keys_pass_tuning_through():
+    """engine:<key>=<int> (an extension: the engine's artes_set_tuning keys, e.g. det_ordered)."""
+    c = RunConfig()
+    c.apply("engine:det_ordered", "1")
+    c.apply("engine:trace_gtab", "0")
+    assert c.engine == {"det_ordered": 1, "trace_gtab": 0}
+    d = c.copy()
+    d.apply("engine:det_ordered", "0")
+    assert c.engine["det_ordered"] == 1 and d.engine["det_ordered"] == 0
+    with pytest.raises(ConfigError):
+        RunConfig().apply("engine:det_ordered", "on")
 
 
 def test_line_rules(tmp_path):

@@ -35,7 +35,16 @@ def transport(first, n, seed):
 res = dist.run_sharded(transport, 30001, 99, r)
 seed = dist.broadcast_int((2**62 + 12345) if r.rank == 0 else 777, r)   # the CLI's clock seed
 open({out!r}.replace("det2.npy", "seed%d.txt" % r.rank), "w").write(str(seed))
+# an unsharded call (world 1) inside this 2-rank group: not reduced (ADVICE r05)
+solo = dist.run_sharded(transport, 5000, 7, dist.Rank(r.rank, 1, r.local_rank))
+try:
+    dist.reduces(3)
+    mismatch = "accepted"
+except RuntimeError:
+    mismatch = "refused"
 if r.rank == 0:
+    np.save({out!r}.replace(".npy", "_solo.npy"), solo.det)
+    open({out!r}.replace("det2.npy", "mismatch.txt"), "w").write(mismatch)
     open({out!r}.replace("det2.npy", "backend.txt"), "w").write(tdist.get_backend())
     np.save({out!r}, res.det)
     np.save({out!r}.replace(".npy", "_cnt.npy"), res.counters)
@@ -82,6 +91,10 @@ def test_two_rank_gloo_equals_single_process(tmp_path):
     # the flow diagnostics are summed over the ranks too
     np.testing.assert_allclose(np.load(out.replace(".npy", "_flow.npy")), fg1, rtol=1e-10, atol=1e-12 * np.abs(fg1).max())
     np.testing.assert_allclose(np.load(out.replace(".npy", "_lat.npy")), ft1, rtol=1e-11, atol=1e-300)
+    # a world-1 call inside the group transports all its packets on each rank and is not summed
+    d_solo = g.run_flow(p, 0, 5000, 7, threads=4)[0]
+    np.testing.assert_allclose(np.load(out.replace(".npy", "_solo.npy")), d_solo, rtol=1e-11, atol=1e-300)
+    assert open(str(tmp_path / "mismatch.txt")).read() == "refused"
 
 
 def test_device_of_is_local_rank_modulo_visible_devices(monkeypatch):

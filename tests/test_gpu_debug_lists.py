@@ -54,7 +54,7 @@ print(json.dumps(dict(err=[int(e) for e in r.err], cnt=[int(c) for c in r.counte
 
 
 def _run(lib, case):
-    env = dict(os.environ, ARTES_LIB_PATH=lib)
+    env = dict(os.environ, ARTES_LIB_PATH=lib, ARTES_DEV_LIB="1")
     out = subprocess.run([sys.executable, "-c", SCRIPT.format(root=ROOT), json.dumps(case)], capture_output=True,
                          text=True, timeout=120, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
@@ -109,7 +109,7 @@ except EngineError as e:
     print(json.dumps(dict(failed=True, e61=int(e.err[61]), e62=int(e.err[62]))))
 """.format(root=ROOT)
     out = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=120,
-                         env=dict(os.environ, ARTES_LIB_PATH=lib), cwd=ROOT)
+                         env=dict(os.environ, ARTES_LIB_PATH=lib, ARTES_DEV_LIB="1"), cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["failed"] and r["e61"] > 0 and r["e62"] > 0, r

@@ -53,6 +53,25 @@ def test_launch_knobs_do_not_change_results(require_gpu, knobs):
     np.testing.assert_allclose(base.totals, other.totals, rtol=1e-9)
 
 
+def test_pool_key_shrinks_an_existing_pool_and_last_launch_names_the_engine(require_gpu, capfd):
+    """The "pool" key takes effect on a grid that already holds a larger pool (it is
+    reallocated), and artes_last_launch reports "none" for a call that launched nothing
+    (ADVICE r05)."""
+    atm, grid, p = _setup("hg")
+    grid.set_tuning(verbose=1)
+    base = grid.run(p, 0, 300000, 99)
+    grid.set_tuning(pool=5000)
+    other = grid.run(p, 0, 300000, 99)
+    err = capfd.readouterr().err
+    pools = [int(l.split("pool ")[1].split(",")[0]) for l in err.splitlines() if "event engine: pool" in l]
+    assert len(pools) == 2 and pools[0] > 5000 >= pools[1] - 1023, err
+    np.testing.assert_array_equal(base.counters, other.counters)
+    np.testing.assert_allclose(base.det, other.det, rtol=1e-9, atol=1e-300)
+    assert grid.last_launch().startswith("k_trace<0,0,4,0,8>")
+    grid.run(p, 0, 0, 99)
+    assert grid.last_launch() == "none"
+
+
 @pytest.mark.parametrize("name,spec", [("hg", {}), ("ray3d", dict(nr=10, ntheta=6, nphi=8, tau=3.0))])
 def test_backward_propagation_matches_forward(require_gpu, name, spec):
     """The propagation after the forced first interaction may walk the chord back from

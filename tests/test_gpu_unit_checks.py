@@ -210,6 +210,7 @@ def test_scatter_geometry_matches_angle_forms(det_theta, det_phi):
     det = [math.sin(det_theta) * math.cos(det_phi), math.sin(det_theta) * math.sin(det_phi), math.cos(det_theta)]
     ref_errs = []
     worst_dir = worst_stokes = 0.0
+    n_boundary = clamped = 0
     wd_case = ws_case = None
     for i in range(n):
         d = cases[i, :3]
@@ -221,12 +222,13 @@ def test_scatter_geometry_matches_angle_forms(det_theta, det_phi):
         dd = max(abs(a - b) for a, b in zip(e, out[i, :3]))
         # num = +-1 in exact arithmetic (beta = 0 or pi: the new direction in the old one's
         # meridian plane) is the clamp's boundary: the reference moves the azimuth by
-        # acos(1 - 1e-10) = 1.4e-5 rad when num rounds to >= 1 and by ~1e-8 when it rounds below,
-        # so either form may take either side (the device's fused multiply-adds round it
-        # differently).  There the device must match the reference on one of the two sides.
-        if dd > 1e-9 and abs(abs(_num(cases[i, 3], cases[i, 4], d)) - 1.0) < 1e-9:
-            dd = min(max(abs(a - b) for a, b in zip(_direction_cosine(cases[i, 3], cases[i, 4], d, [], clamp=c), out[i, :3]))
-                     for c in (True, False))
+        # acos(1 - 1e-10) = 1.4e-5 rad when num rounds to >= 1 and by ~1e-8 when it rounds below.
+        # The device evaluates num as the reference does (no fused multiply-adds, correctly
+        # rounded roots: device_common.hpp, direction_cosine_cs), so it must take the
+        # reference's side there too: no either-side escape.
+        if abs(abs(_num(cases[i, 3], cases[i, 4], d)) - 1.0) < 1e-9:
+            n_boundary += 1
+            clamped += abs(_num(cases[i, 3], cases[i, 4], d)) >= 1.0
         dd /= scale
         if dd > worst_dir:
             worst_dir, wd_case = dd, (list(cases[i]), e, list(out[i, :3]))
@@ -250,6 +252,7 @@ def test_scatter_geometry_matches_angle_forms(det_theta, det_phi):
     # (phi_new ~ 0 / pi, phs ~ 0 / pi) carries ~1e-8, and the 1e-10 clamps of num 5e-10
     # (near-vertical directions: scaled by their conditioning, above)
     assert worst_dir < 1e-7, (worst_dir, wd_case)
+    assert n_boundary > 0 and clamped > 0, (n_boundary, clamped)   # (the clamp's side is exercised)
     assert worst_stokes < 1e-7, (worst_stokes, ws_case)
     for code in (44, 45, 49):
         assert int(err[code]) == ref_errs.count(code), (code, int(err[code]), ref_errs.count(code))

@@ -2,6 +2,7 @@
 # Lane accounting (-DARTES_DEBUG_LANES) and region timing (-DARTES_DEBUG_TIMING) of k_trace on
 # ray3d and the cloudy phase call (development tool).
 # usage (via gpurun): bash tools/gpu_lanes_regions.sh <out> [packets]
+export ARTES_DEV_LIB=1   # (development builds load only with this opt-in: artes_amd/engine.py)
 set -o pipefail
 O=gpurun_out/$1; mkdir -p $O
 N=${2:-1e8}

@@ -1,6 +1,7 @@
 #!/bin/bash
 # k_trace region timing (the -DARTES_DEBUG_TIMING build) on ray3d and the cloudy calls.
 # usage (via gpurun): bash tools/gpu_time_regions.sh <out> [packets] [ENV=V,...]...
+export ARTES_DEV_LIB=1   # (development builds load only with this opt-in: artes_amd/engine.py)
 set -o pipefail
 O=gpurun_out/$1; shift; mkdir -p $O
 N=${1:-1e8}; shift
