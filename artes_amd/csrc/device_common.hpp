@@ -627,14 +627,30 @@ __device__ __forceinline__ int cdf_search4(double s, F cdf) {
     return lo;
 }
 
+// The cumulative tables' element (j, k) (entry j = 0..180, column k = 0..3): [181][4] in global
+// memory (CS = 4); in LDS (CS = 5) entries padded to 5 doubles.  ARTES_CUM_LAYOUT (A/B builds,
+// profiles/r06/ab/event_lds_layout_ab.txt): 1 the four columns as separate arrays of 182, 2 the
+// padded entries at an XOR-swizzled row j ^ ((j >> 4) & 15) (192 rows).
+#ifndef ARTES_CUM_LAYOUT
+#define ARTES_CUM_LAYOUT 0
+#endif
+template <int CS>
+__host__ __device__ __forceinline__ int cum_at(int j, int k) {
+    if constexpr (CS == 4 || ARTES_CUM_LAYOUT == 0) return j * CS + k;
+    else if constexpr (ARTES_CUM_LAYOUT == 1) return k * 182 + j;
+    else return (j ^ ((j >> 4) & 15)) * CS + k;
+}
+// doubles per LDS cumulative table of the layout
+constexpr int cum_lds_doubles() { return ARTES_CUM_LAYOUT == 1 ? 4 * 182 : ARTES_CUM_LAYOUT == 2 ? 192 * 5 : 181 * 5; }
+
 // scattering_angle_sampling (ARTES.f90:1534-1661) by searching the cumulative tables;
-// C = [181][CS] (CS = 4, or 5 in LDS: see k_event)
+// C = [181][CS] (CS = 4, or 5 in LDS: see k_event, cum_at)
 template <int CS = 4>
 __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* __restrict__ C, Rng& rng,
                               const double st[4], double& alpha, double& beta, double& c2b, double& s2b,
                               double* adeg_out = nullptr) {
     // azimuth: C_b(i) = i (p11 I + p14 V) + (p12 Q + p13 U) SC2(i) + (p12 U - p13 Q) SS2(i)
-    const double p11 = C[180 * CS + 0], p12 = C[180 * CS + 1], p13 = C[180 * CS + 2], p14 = C[180 * CS + 3];
+    const double p11 = C[cum_at<CS>(180, 0)], p12 = C[cum_at<CS>(180, 1)], p13 = C[cum_at<CS>(180, 2)], p14 = C[cum_at<CS>(180, 3)];
     const double u = p11 * st[0] + p14 * st[3];
     const double v = p12 * st[1] + p13 * st[2];
     const double w = p12 * st[2] - p13 * st[1];
@@ -655,8 +671,7 @@ __device__ void sample_angles(const DevGrid& G, const DevRun& R, const double* _
     // polar: C_t(i) = I A1(i) + (c2b Q + s2b U) A2(i) + (c2b U - s2b Q) A3(i) + V A4(i)
     const double k0 = st[0], k1 = c2b * st[1] + s2b * st[2], k2 = c2b * st[2] - s2b * st[1], k3 = st[3];
     auto ct = [&](int j) {
-        const double* a = C + j * CS;
-        return k0 * a[0] + k1 * a[1] + k2 * a[2] + k3 * a[3];
+        return k0 * C[cum_at<CS>(j, 0)] + k1 * C[cum_at<CS>(j, 1)] + k2 * C[cum_at<CS>(j, 2)] + k3 * C[cum_at<CS>(j, 3)];
     };
     s = rng.uni() * ct(180);
 #ifdef ARTES_SEARCH2

@@ -625,7 +625,7 @@ struct TabLayout {
     static constexpr int RS4 = PAD ? 5 : 4;             // row stride of the symmetric form (DevGrid::msym)
     static constexpr int MAT4 = NANG * RS4;
     static constexpr int CS = PAD ? 5 : 4;              // cumulative-table entry stride
-    static constexpr int CUM = (NANG + 1) * CS;         // doubles per cumulative table
+    static constexpr int CUM = PAD ? cum_lds_doubles() : (NANG + 1) * CS;   // doubles per cumulative table (cum_at)
 };
 
 // Development timing build (-DARTES_DEBUG_TIMING): shader-clock cycles of k_event's regions,
@@ -838,7 +838,10 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         double* c = s_ev;
         double* a = c + G0.nmat * TL::CUM;
         double* b = a + (NANG + 1);
-        for (int i = threadIdx.x; i < nc; i += EB) c[(i >> 2) * TL::CS + (i & 3)] = G0.cums[i];    // entries of 4 -> 5
+        for (int i = threadIdx.x; i < nc; i += EB) {   // entries of 4 -> 5 (cum_at)
+            const int e = i >> 2, mm = e / (NANG + 1);
+            c[mm * TL::CUM + cum_at<TL::CS>(e - mm * (NANG + 1), i & 3)] = G0.cums[i];
+        }
         for (int i = threadIdx.x; i <= NANG; i += EB) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
         G.cums = c; G.sc2 = a; G.ss2 = b;
         lds_next = b + (NANG + 1);
@@ -855,7 +858,10 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         } else {
             for (int i = threadIdx.x; i < G0.nmat * MAT_DOUBLES; i += EB) m[(i >> 4) * TL::RS + (i & 15)] = G0.mats[i];   // rows of 16 -> 17
         }
-        for (int i = threadIdx.x; i < nc; i += EB) c[(i >> 2) * TL::CS + (i & 3)] = G0.cums[i];    // entries of 4 -> 5
+        for (int i = threadIdx.x; i < nc; i += EB) {   // entries of 4 -> 5 (cum_at)
+            const int e = i >> 2, mm = e / (NANG + 1);
+            c[mm * TL::CUM + cum_at<TL::CS>(e - mm * (NANG + 1), i & 3)] = G0.cums[i];
+        }
         for (int i = threadIdx.x; i <= NANG; i += EB) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
         G.mats = m; G.cums = c; G.sc2 = a; G.ss2 = b;
         lds_next = b + (NANG + 1);

@@ -117,18 +117,25 @@ __device__ __forceinline__ double fast_sqrt_nan0(double x) {
 // thresholds live in them.  (The inline move makes them opaque: the compiler cannot fold them back.)
 struct TraceK {
     double tiny, tol, tol_same, huge, cap, step_min, inf;   // 1e-100 1e-15 1e-3 1e100 1e300 1e-9 inf
+    int nan_hi;                                             // 0x7FF80000: a quiet NaN's high word (or_nan)
 };
 __device__ __forceinline__ double vreg(double c) {
     double r;
     asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "s"(c));
     return r;
 }
+__device__ __forceinline__ int vreg_i(int c) {
+    int r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(c));
+    return r;
+}
 template <bool IN_VGPRS>
 __device__ __forceinline__ TraceK trace_consts() {
     if constexpr (IN_VGPRS)
-        return TraceK{vreg(1.e-100), vreg(1.e-15), vreg(1.e-3), vreg(1.e100), vreg(1.e300), vreg(1.e-9), vreg(__builtin_inf())};
+        return TraceK{vreg(1.e-100), vreg(1.e-15), vreg(1.e-3), vreg(1.e100), vreg(1.e300), vreg(1.e-9), vreg(__builtin_inf()),
+                      vreg_i(0x7FF80000)};
     else
-        return TraceK{1.e-100, 1.e-15, 1.e-3, 1.e100, 1.e300, 1.e-9, __builtin_inf()};
+        return TraceK{1.e-100, 1.e-15, 1.e-3, 1.e100, 1.e300, 1.e-9, __builtin_inf(), 0x7FF80000};
 }
 
 // ---------------------------------------------------- face tables (LDS) ---
@@ -228,7 +235,9 @@ constexpr double INF = __builtin_inf();
 // k_trace's `parked` codes: 1 (3 after a cell error) the forced first interaction waits, 4 the
 // interaction waits; PK_END and its bits (trace-relative kernels): a trace end found in a step,
 // resolved at the end of the iteration
-enum : int { PK_END = 8, PK_EXIT = 16, PK_SURF = 32, PK_ERR31 = 64, PK_RUNAWAY = 128, PK_ERR = 256 };
+// PK_RAD: a trace end of the radial-form step, whose exit / surface / runaway bits the end block
+// derives from the state (tfi the sphere crossed, ncross against nlim) instead of the step
+enum : int { PK_END = 8, PK_EXIT = 16, PK_SURF = 32, PK_ERR31 = 64, PK_RUNAWAY = 128, PK_ERR = 256, PK_RAD = 512 };
 // a new trace's set-up (k_trace's common set-up block): the start cell from the packet position,
 // the direction's constants
 enum : int { NT_POS = 1, NT_DIR = 2 };
@@ -238,6 +247,10 @@ enum : int { NT_POS = 1, NT_DIR = 2 };
 // a NaN distance means "no crossing" as +inf does.
 __device__ __forceinline__ double or_nan(bool valid, double x) {
     return __hiloint2double(valid ? __double2hiint(x) : 0x7FF80000, __double2loint(x));
+}
+// the same with the NaN's high word from a register (gfx950's VOP3 select takes no literal)
+__device__ __forceinline__ double or_nan(bool valid, double x, int nan_hi) {
+    return __hiloint2double(valid ? __double2hiint(x) : nan_hi, __double2loint(x));
 }
 
 // the scaled squared length of a direction's xy part (one expression for every caller, so
@@ -532,7 +545,7 @@ __device__ __forceinline__ double radial_next(const double2 rr, double b0, doubl
     const bool ok = dA != dB;
     const bool vA = ok & (dA > tmin), vB = ok & (dB > tmin);
     outer = ch;
-    return min_nonan(or_nan(vA, sA), or_nan(vB, sB));
+    return min_nonan(or_nan(vA, sA, K.nan_hi), or_nan(vB, sB, K.nan_hi));
 }
 
 // ---------------------------------------------- phi family, trace-relative (TREL) ---
@@ -1103,7 +1116,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         // ray3d 3 %.)
         // Trace-relative kernels: NREP steps in the radial form (a sphere beyond 1e-9 m: ~99.9 % of
         // the crossings on the bench grid, 99.6 % on the cloudy one), then one generic step for
-        // every family and the reference's two-pass choice.  A lane whose next crossing is a
+        // every family and the reference's two-pass choice.  (The generic slot taking the fused
+        // radial step for its radial lanes too measured slower: ray3d k_trace +1.7 %, hg +1.6 %,
+        // profiles/r06/ab/trace_mixed_generic_slot_ab.txt.)  A lane whose next crossing is a
         // theta / phi face, or lies within 1e-9 m, waits for that last step of the iteration: the
         // radial form is then a straight sequence of instructions with no per-lane choice of the
         // crossed family's index, no phi wrap and no index selects, and no join of two step forms
@@ -1364,8 +1379,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         sides = (sides & ~1) | (outer ? 1 : 0);
                         pending |= (dm < K.inf) ? 0 : 1;   // (NaN: radial_tr in the next slot, alt)
                     } else {
-                        parked = hitpark ? 4 : (PK_END | (exit ? PK_EXIT : 0) | (surf ? PK_SURF : 0) | (runaway ? PK_ERR31 | PK_RUNAWAY : 0) |
-                                                (err ? PK_ERR : 0));
+                        // (the end's reasons follow from the state at the end of the iteration: PK_RAD)
+                        parked = hitpark ? 4 : (PK_END | PK_RAD | (err ? PK_ERR : 0));
                     }
                 }   // rstep
             } else if (do_step) {
@@ -1556,8 +1571,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             // unchanged.)
             if (__ballot(parked >= PK_END)) {
                 if (parked >= PK_END) {
-                    const int sk = parked;
+                    int sk = parked;
                     parked = 0;
+                    if (sk & PK_RAD) {
+                        // the radial-form step (ARTES.f90:2885-3010 faces): the packet crossed sphere tfi
+                        // (tft = 1); a runaway is the crossing count past nlim (it was counted), exit the
+                        // top sphere and the surface sphere cell_depth otherwise
+                        const bool runaway = (sk & PK_ERR) && ncross > nlim;
+                        sk |= runaway ? (PK_ERR31 | PK_RUNAWAY) : ((tfi == G.nr ? PK_EXIT : 0) | (tfi == G.cell_depth ? PK_SURF : 0));
+                    }
                     const bool exit = (sk & PK_EXIT) != 0, surf = (sk & PK_SURF) != 0, err = (sk & PK_ERR) != 0;
                     if (err) {
                         if (sk & PK_RUNAWAY) log_err(R, ARTES_ERR_RUNAWAY);

@@ -115,6 +115,9 @@ def main() -> int:
     ap.add_argument("--no-variants", action="store_true", help="skip the untimed configs[2] (32x16x32) leg (profiling passes)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05", "pmc_summary.json"))
     ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r05", "pmc_sq_summary.json"))
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="an artes_set_tuning override of the bench grid (measurements only, e.g. det_ordered=1; "
+                         "reported under engine.tuning)")
     args = ap.parse_args()
 
     import numpy as np
@@ -138,6 +141,9 @@ def main() -> int:
     rtop = float(atm["radial"][-1])
     det_geom = driver.detector_geometry(cfg, rtop)
     grid = Grid(atm, device=dev)
+    for kv in args.tune:
+        k, v = kv.split("=", 1)
+        grid.set_tuning(**{k: int(v)})
     # the timed steps run the drop-in's production configuration: no packet-level moments
     # (the reference has none); the parity check below reruns one step with them
     params = driver.run_params(cfg, det_geom, 0, cell_depth=grid.cell_depth(0), packet_moments=False)
