@@ -493,20 +493,28 @@ struct DetAcc {
     double* __restrict__ det;
     double* __restrict__ acc;
     size_t plane;
-    double* __restrict__ lane;   // PIX1: this lane's slot, lane[k * stride]
+    double* __restrict__ lane;   // PIX1: this lane's slot, lane[k * stride] (planes 0-7)
     int stride;
+    uint32_t n8;                 // PIX1: the lane's peel count (plane 8 adds 1 per peel): a register
     unsigned long long* __restrict__ fix;   // DM_ORD: the block's fixed-point copy
     __device__ __forceinline__ void init(double* d, double* a, size_t pl, double* slots = nullptr, int nthreads = 0,
                                          unsigned long long* f = nullptr) {
         det = d; acc = a; plane = pl; fix = f;
+        n8 = 0;
         if constexpr (DM == DM_PIX1) {
             lane = slots + threadIdx.x; stride = nthreads;
 #pragma unroll
-            for (int k = 0; k < 10; k++) lane[k * stride] = 0.0;
+            for (int k = 0; k < 8; k++) lane[k * stride] = 0.0;
         }
     }
+    // (plane 8 takes v = 1 at its call site: a peel's count; plane 9 -- the I-only count of the
+    // rare thermal / surface peels -- goes to the HBM copy at once)
     __device__ __forceinline__ void add(int k, int pix, double v) {
-        if constexpr (DM == DM_PIX1) lane[k * stride] += v;
+        if constexpr (DM == DM_PIX1) {
+            if (k == 8) n8++;
+            else if (k == 9) unsafeAtomicAdd(&det[9 * plane], v);
+            else lane[k * stride] += v;
+        }
         else if constexpr (DM == DM_ORD) fix_add(fix + 2 * ((size_t)k * plane + pix), v);
         else if (k == 9) unsafeAtomicAdd(&det[9 * plane + pix], v);   // rare (thermal / surface)
         else unsafeAtomicAdd(&acc[k * plane + pix], v);
@@ -515,16 +523,16 @@ struct DetAcc {
     __device__ __forceinline__ void flush_wave() {
         if constexpr (DM == DM_PIX1) {
 #pragma unroll
-            for (int k = 0; k < 10; k++) {
-                const double v = wave_sum_f64(lane[k * stride]);
+            for (int k = 0; k < 9; k++) {
+                const double v = k < 8 ? wave_sum_f64(lane[k * stride]) : (double)wave_sum_u64(n8);
                 if ((threadIdx.x & 63) == 0 && v != 0.0) unsafeAtomicAdd(&det[k * plane], v);
             }
         }
     }
 };
 
-// LDS bytes of the PIX1 per-lane slots of a k_event block
-__host__ __device__ inline size_t pix1_slot_bytes(int block) { return (size_t)10 * block * sizeof(double); }
+// LDS bytes of the PIX1 per-lane slots of a k_event block (planes 0-7; the counts are registers)
+__host__ __device__ inline size_t pix1_slot_bytes(int block) { return (size_t)8 * block * sizeof(double); }
 
 // a peel that carries Stokes I only (peel_thermal 4577-4583, peel_surface 4684-4690):
 // moments 0 and 4, and the I-only count plane 9 (the reference counts it for I alone)
@@ -789,6 +797,10 @@ __device__ __forceinline__ int event_one(const DevGrid& G, const DevRun& R, cons
 __host__ __device__ inline size_t event_table_doubles(int nmat, bool sym) {
     return (size_t)nmat * ((sym ? TabLayout<true>::MAT4 : TabLayout<true>::MAT) + TabLayout<true>::CUM) + 2 * (NANG + 1);
 }
+// the same unpadded (k_event TPAD = false: the global layout)
+__host__ __device__ inline size_t event_table_doubles_unpadded(int nmat, bool sym) {
+    return (size_t)nmat * ((sym ? NANG * 4 : MAT_DOUBLES) + CUM_DOUBLES) + 2 * (NANG + 1);
+}
 // the same for the cumulative tables and the azimuth tables alone (LDS_C)
 __host__ __device__ inline size_t event_cum_doubles(int nmat) {
     return (size_t)nmat * TabLayout<true>::CUM + 2 * (NANG + 1);
@@ -820,11 +832,16 @@ static constexpr bool EV_PREFETCH = ARTES_EV_PREFETCH != 0;
 //         L2.  (The call's matrices are its wavelength's only: the host remaps matrix ids
 //         per wavelength, transport.hip, wl_set.)
 //  ORD:   planes 0-9 as 128-bit fixed-point integers (DetAcc DM_ORD; tuning "det_ordered"):
-//         bit-reproducible detector images, no LDS detector or per-lane sums.
-template <bool LDS_T, bool LDS_D, bool PIX1 = false, int EB = BLOCK, bool LDS_C = false, bool ORD = false>
+//         bit-reproducible detector images, no LDS detector or per-lane sums.  1: added to the
+//         block's HBM copy at once; 2: accumulated in LDS (integer LDS atomics) and added to the
+//         HBM copy at the end of the block (128-bit adds of the block's sums: still exact).
+//  TPAD:  (with LDS_T) the tables in LDS padded against bank conflicts (17 / 5 doubles per row) or,
+//         when only that fits, unpadded -- the global layout (the cloudy calls' 9 matrices per
+//         wavelength: 104 KB unpadded beside the one-pixel lane slots, 130 KB padded)
+template <bool LDS_T, bool LDS_D, bool PIX1 = false, int EB = BLOCK, bool LDS_C = false, int ORD = 0, bool TPAD = true>
 __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_WPE, 8))) void k_event(DevGrid G0, DevRun R, Pool S, SubLists SL) {
     static_assert(!(PIX1 && LDS_D), "a one-pixel detector is reduced per lane");
-    static_assert(!(ORD && (PIX1 || LDS_D)), "the ordered detector is accumulated in integers in HBM");
+    static_assert(!(ORD && (PIX1 || LDS_D)), "the ordered detector is accumulated in integers");
     constexpr int DM = ORD ? DM_ORD : (PIX1 ? DM_PIX1 : DM_ATOM);
     static_assert(!(LDS_T && LDS_C), "LDS_C stages the cumulative tables alone");
     const Lists L = SL.l[sub_of_block()];
@@ -846,7 +863,19 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         G.cums = c; G.sc2 = a; G.ss2 = b;
         lds_next = b + (NANG + 1);
     }
-    if constexpr (LDS_T) {
+    if constexpr (LDS_T && !TPAD) {   // the global layout, copied
+        const int nm = G0.nmat * (G0.msym ? NANG * 4 : MAT_DOUBLES), nc = G0.nmat * CUM_DOUBLES;
+        double* m = s_ev;
+        double* c = m + nm;
+        double* a = c + nc;
+        double* b = a + (NANG + 1);
+        for (int i = threadIdx.x; i < nm; i += EB) m[i] = G0.mats[i];
+        for (int i = threadIdx.x; i < nc; i += EB) c[i] = G0.cums[i];
+        for (int i = threadIdx.x; i <= NANG; i += EB) { a[i] = G0.sc2[i]; b[i] = G0.ss2[i]; }
+        G.mats = m; G.cums = c; G.sc2 = a; G.ss2 = b;
+        lds_next = b + (NANG + 1);
+    }
+    if constexpr (LDS_T && TPAD) {
         using TL = TabLayout<true>;
         const int nc = G0.nmat * CUM_DOUBLES;
         double* m = s_ev;
@@ -872,9 +901,15 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
         acc = lds_next;
         for (size_t i = threadIdx.x; i < 9 * plane; i += EB) acc[i] = 0.0;
     }
-    if constexpr (LDS_T || LDS_D || LDS_C) __syncthreads();
+    unsigned long long* __restrict__ fix_hbm = ORD ? R.fix + (size_t)(blockIdx.x % R.nfix) * R.fix_stride : nullptr;
+    unsigned long long* __restrict__ fix = fix_hbm;
+    if constexpr (ORD == 2) {   // the block's fixed-point planes 0-9 in LDS
+        fix = (unsigned long long*)lds_next;
+        for (size_t i = threadIdx.x; i < 20 * plane; i += EB) fix[i] = 0ull;
+    }
+    if constexpr (LDS_T || LDS_D || LDS_C || ORD == 2) __syncthreads();
     DetAcc<DM> D;
-    D.init(det, acc, plane, lds_next, EB, ORD ? R.fix + (size_t)(blockIdx.x % R.nfix) * R.fix_stride : nullptr);
+    D.init(det, acc, plane, lds_next, EB, fix);
     const int n = *L.event_n;
     uint32_t c_scat = 0, c_det = 0;
     const int n_pad = (n + 63) & ~63;   // whole waves iterate together (wave-aggregated appends)
@@ -907,9 +942,9 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
 #endif
         EV_TICK(te0);
 #ifdef ARTES_DEBUG_TIMING
-        const int dest = slot >= 0 ? event_one<DM, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det, ev_tm) : 0;
+        const int dest = slot >= 0 ? event_one<DM, LDS_T && TPAD, (LDS_T && TPAD) || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det, ev_tm) : 0;
 #else
-        const int dest = slot >= 0 ? event_one<DM, LDS_T, LDS_T || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
+        const int dest = slot >= 0 ? event_one<DM, LDS_T && TPAD, (LDS_T && TPAD) || LDS_C>(G, R, S, slot, cur, D, c_scat, c_det) : 0;
 #endif
         EV_TICK(te1);
         EV_ADD(21, te1 - te0);
@@ -941,6 +976,15 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(ARTES_EVENT_
     if ((threadIdx.x & 63) >= 20 && (threadIdx.x & 63) < 28) atomicAdd(&R.err[threadIdx.x & 63], ev_tm[threadIdx.x & 63]);
 #endif
     D.flush_wave();
+    if constexpr (ORD == 2) {   // the block's integer sums into its HBM copy, 128 bits each
+        __syncthreads();
+        for (size_t i = threadIdx.x; i < 10 * plane; i += EB) {
+            const unsigned long long lo = fix[2 * i], hi = fix[2 * i + 1];
+            if ((lo | hi) == 0) continue;
+            const unsigned long long old = atomicAdd(fix_hbm + 2 * i, lo);
+            atomicAdd(fix_hbm + 2 * i + 1, hi + (old + lo < old ? 1ull : 0ull));
+        }
+    }
     if constexpr (LDS_D) {
         __syncthreads();
         for (size_t i = threadIdx.x; i < 9 * plane; i += EB) {

@@ -126,7 +126,7 @@ using namespace artes;
 enum TuneKey : int {
     T_ENGINE, T_POOL, T_STEPS, T_REFILL, T_STATIC, T_DGRAB, T_BATCH, T_BATCH_MIN, T_HBATCH, T_GBATCH, T_DEFER,
     T_BACKWARD, T_EMIT_FIRST, T_LATE_APPEND, T_PIX1, T_DET_LDS, T_EVENT_LDS, T_EVENT_LDSC, T_EVENT_BLOCK, T_EVENT_BPC,
-    T_TRACE_BPC, T_WPE, T_MSYM, T_MAX_IT, T_VERBOSE, T_TRACE_GTAB, T_DET_ORDERED, T_NUM
+    T_TRACE_BPC, T_WPE, T_MSYM, T_MAX_IT, T_VERBOSE, T_TRACE_GTAB, T_DET_ORDERED, T_EVENT_LDSU, T_NUM
 };
 struct TuneSpec {
     const char* name;
@@ -160,6 +160,7 @@ static const TuneSpec TUNE[T_NUM] = {
     {"verbose", 0, 1},           // one stderr line per call (pool, iterations, kernel choice)
     {"trace_gtab", 0, 1},        // k_trace's face tables in global memory (automatic beyond 64 KiB)
     {"det_ordered", 0, 1},       // detector partials summed in a fixed order: bit-reproducible images
+    {"event_ldsu", 0, 1},        // k_event tables in LDS unpadded when only that fits
 };
 
 struct artes_grid {
@@ -782,22 +783,52 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     else if (ev_lds) ev_v = 10;
     else if (det_lds && ev_block == EVB) ev_v = 11;
     else if (det_lds) ev_v = 12;
+    // the call's tables too many for LDS padded but not unpadded (the global layout: the cloudy
+    // calls' 9 matrices per wavelength, 104 KB against 130 KB padded) beside the one-pixel lane
+    // slots or the LDS detector: k_event TPAD = false instead of the cumulative tables alone
+    // (tuning "event_ldsu" = 0 turns it off; profiles/r06/ab/event_tables_unpadded_ab.txt)
+    const size_t evu_bytes = event_table_doubles_unpadded(G.nmat, G.msym != 0) * sizeof(double);
+    if (!ev_lds && ev_block == EVB && tv(g, T_EVENT_LDS, 1) != 0 && tv(g, T_EVENT_LDSU, 1) != 0) {
+        if (pix1_big && evu_bytes + pix1_slot_bytes(EVB) <= lds_cap) {
+            ev_v = 17;
+            ev_blocks = round_sub(blocks_per_cu(g, k_event<true, false, true, EVB, false, 0, false>,
+                                                evu_bytes + pix1_slot_bytes(EVB), EVB) * g->num_cus);
+        } else if (det_lds && evu_bytes + det_bytes <= lds_cap) {
+            ev_v = 18;
+            ev_blocks = round_sub((int)tv(g, T_EVENT_BPC, blocks_per_cu(g, k_event<true, true, false, EVB, false, 0, false>,
+                                                                         evu_bytes + det_bytes, EVB)) * g->num_cus);
+        }
+    }
     // det_ordered: the fixed-point detector (k_event ORD), EVB-thread blocks, the tables in LDS as
     // far as they fit alone
+    // (the block's integer sums in LDS when they fit beside the tables -- 160 B per pixel: 25 x 25
+    // imaging 100 KB, a one-pixel detector 160 B -- else added to the HBM copy at once)
+    const size_t fixl_bytes = 20 * (size_t)R.nx * R.ny * sizeof(unsigned long long);
+    const bool ord_ldsc = cum_bytes <= lds_cap && tv(g, T_EVENT_LDSC, 1) != 0;
     if (R.fix) {
-        ev_v = ev_lds ? 14 : (cum_bytes <= lds_cap && tv(g, T_EVENT_LDSC, 1) != 0) ? 15 : 16;
-        ev_blocks = round_sub((ev_v == 14 ? blocks_per_cu(g, k_event<true, false, false, EVB, false, true>, ev_bytes, EVB)
-                               : ev_v == 15 ? blocks_per_cu(g, k_event<false, false, false, EVB, true, true>, cum_bytes, EVB)
-                                            : blocks_per_cu(g, k_event<false, false, false, EVB, false, true>, 0, EVB)) * g->num_cus);
+        if (ev_lds && ev_bytes + fixl_bytes <= lds_cap) ev_v = 14;
+        else if (ord_ldsc && cum_bytes + fixl_bytes <= lds_cap) ev_v = 15;
+        else if (fixl_bytes <= lds_cap) ev_v = 16;
+        else ev_v = ord_ldsc ? 19 : 20;
+        ev_blocks = round_sub((ev_v == 14 ? blocks_per_cu(g, k_event<true, false, false, EVB, false, 2>, ev_bytes + fixl_bytes, EVB)
+                               : ev_v == 15 ? blocks_per_cu(g, k_event<false, false, false, EVB, true, 2>, cum_bytes + fixl_bytes, EVB)
+                               : ev_v == 16 ? blocks_per_cu(g, k_event<false, false, false, EVB, false, 2>, fixl_bytes, EVB)
+                               : ev_v == 19 ? blocks_per_cu(g, k_event<false, false, false, EVB, true, 1>, cum_bytes, EVB)
+                                            : blocks_per_cu(g, k_event<false, false, false, EVB, false, 1>, 0, EVB)) * g->num_cus);
     }
-    static const struct { int lt, ld, p1, big, lc; } EVV[17] = {
-        {0, 0, 0, 0, 0}, {1, 0, 1, 1, 0}, {0, 0, 1, 1, 1}, {0, 1, 0, 1, 1}, {0, 0, 0, 1, 1}, {0, 0, 1, 1, 0}, {1, 0, 1, 0, 0},
-        {0, 0, 1, 0, 0}, {1, 1, 0, 1, 0}, {1, 1, 0, 0, 0}, {1, 0, 0, 0, 0}, {0, 1, 0, 1, 0}, {0, 1, 0, 0, 0}, {0, 0, 0, 0, 0},
-        {1, 0, 0, 1, 0}, {0, 0, 0, 1, 1}, {0, 0, 0, 1, 0}};
+    static const struct { int lt, ld, p1, big, lc, ord, tpad; } EVV[21] = {
+        {0, 0, 0, 0, 0, 0, 1}, {1, 0, 1, 1, 0, 0, 1}, {0, 0, 1, 1, 1, 0, 1}, {0, 1, 0, 1, 1, 0, 1}, {0, 0, 0, 1, 1, 0, 1},
+        {0, 0, 1, 1, 0, 0, 1}, {1, 0, 1, 0, 0, 0, 1}, {0, 0, 1, 0, 0, 0, 1}, {1, 1, 0, 1, 0, 0, 1}, {1, 1, 0, 0, 0, 0, 1},
+        {1, 0, 0, 0, 0, 0, 1}, {0, 1, 0, 1, 0, 0, 1}, {0, 1, 0, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 0, 1}, {1, 0, 0, 1, 0, 2, 1},
+        {0, 0, 0, 1, 1, 2, 1}, {0, 0, 0, 1, 0, 2, 1}, {1, 0, 1, 1, 0, 0, 0}, {1, 1, 0, 1, 0, 0, 0}, {0, 0, 0, 1, 1, 1, 1},
+        {0, 0, 0, 1, 0, 1, 1}};
     {
+        // (the template arguments LDS_T, LDS_D, PIX1, block, LDS_C, then ORD and TPAD where they are not the defaults)
+        const auto& V = EVV[ev_v];
         char b[96];
-        snprintf(b, sizeof(b), ev_v >= 14 ? "k_event<%d,%d,%d,%d,%d,1>" : "k_event<%d,%d,%d,%d,%d>", EVV[ev_v].lt, EVV[ev_v].ld,
-                 EVV[ev_v].p1, EVV[ev_v].big ? EVB : BLOCK, EVV[ev_v].lc);
+        if (!V.tpad) snprintf(b, sizeof(b), "k_event<%d,%d,%d,%d,%d,%d,0>", V.lt, V.ld, V.p1, V.big ? EVB : BLOCK, V.lc, V.ord);
+        else if (V.ord) snprintf(b, sizeof(b), "k_event<%d,%d,%d,%d,%d,%d>", V.lt, V.ld, V.p1, V.big ? EVB : BLOCK, V.lc, V.ord);
+        else snprintf(b, sizeof(b), "k_event<%d,%d,%d,%d,%d>", V.lt, V.ld, V.p1, V.big ? EVB : BLOCK, V.lc);
         g->last_event = b;
     }
     auto launch_event = [&](const SubLists& L) {
@@ -814,9 +845,13 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
         case 10: hipLaunchKernelGGL((k_event<true, false>), dim3(side_blocks), dim3(BLOCK), ev_bytes, stream, G, R, g->pool, L); break;
         case 11: hipLaunchKernelGGL((k_event<false, true, false, EVB>), dim3(ev_blocks), dim3(EVB), det_bytes, stream, G, R, g->pool, L); break;
         case 12: hipLaunchKernelGGL((k_event<false, true>), dim3(ev_blocks), dim3(BLOCK), det_bytes, stream, G, R, g->pool, L); break;
-        case 14: hipLaunchKernelGGL((k_event<true, false, false, EVB, false, true>), dim3(ev_blocks), dim3(EVB), ev_bytes, stream, G, R, g->pool, L); break;
-        case 15: hipLaunchKernelGGL((k_event<false, false, false, EVB, true, true>), dim3(ev_blocks), dim3(EVB), cum_bytes, stream, G, R, g->pool, L); break;
-        case 16: hipLaunchKernelGGL((k_event<false, false, false, EVB, false, true>), dim3(ev_blocks), dim3(EVB), 0, stream, G, R, g->pool, L); break;
+        case 14: hipLaunchKernelGGL((k_event<true, false, false, EVB, false, 2>), dim3(ev_blocks), dim3(EVB), ev_bytes + fixl_bytes, stream, G, R, g->pool, L); break;
+        case 15: hipLaunchKernelGGL((k_event<false, false, false, EVB, true, 2>), dim3(ev_blocks), dim3(EVB), cum_bytes + fixl_bytes, stream, G, R, g->pool, L); break;
+        case 16: hipLaunchKernelGGL((k_event<false, false, false, EVB, false, 2>), dim3(ev_blocks), dim3(EVB), fixl_bytes, stream, G, R, g->pool, L); break;
+        case 17: hipLaunchKernelGGL((k_event<true, false, true, EVB, false, 0, false>), dim3(ev_blocks), dim3(EVB), evu_bytes + pix1_slot_bytes(EVB), stream, G, R, g->pool, L); break;
+        case 18: hipLaunchKernelGGL((k_event<true, true, false, EVB, false, 0, false>), dim3(ev_blocks), dim3(EVB), evu_bytes + det_bytes, stream, G, R, g->pool, L); break;
+        case 19: hipLaunchKernelGGL((k_event<false, false, false, EVB, true, 1>), dim3(ev_blocks), dim3(EVB), cum_bytes, stream, G, R, g->pool, L); break;
+        case 20: hipLaunchKernelGGL((k_event<false, false, false, EVB, false, 1>), dim3(ev_blocks), dim3(EVB), 0, stream, G, R, g->pool, L); break;
         default: hipLaunchKernelGGL((k_event<false, false>), dim3(side_blocks), dim3(BLOCK), 0, stream, G, R, g->pool, L); break;
         }
     };

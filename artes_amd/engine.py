@@ -29,7 +29,7 @@ KERNEL_NAMES = ("trace", "event", "emit", "aux", "persistent")   # ARTES_K_* ord
 # artes_set_tuning keys (include/artes_amd.h; transport.hip, TUNE)
 TUNING_KEYS = ("engine", "pool", "steps", "refill", "static", "dgrab", "batch", "batch_min", "hbatch", "gbatch", "defer",
                "backward", "emit_first", "late_append", "pix1", "det_lds", "event_lds", "event_ldsc", "event_block",
-               "event_bpc", "trace_bpc", "wpe", "msym", "max_it", "verbose", "trace_gtab", "det_ordered")
+               "event_bpc", "trace_bpc", "wpe", "msym", "max_it", "verbose", "trace_gtab", "det_ordered", "event_ldsu")
 
 
 class EngineUnavailable(RuntimeError):

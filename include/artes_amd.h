@@ -250,7 +250,8 @@ int32_t artes_run_trace(artes_grid* grid, const artes_run_params* params,
  * event_block (256 or 768), event_bpc, trace_bpc, wpe (3 or 4), msym, max_it, verbose,
  * trace_gtab (k_trace's face tables in global memory; automatic when they exceed 64 KiB),
  * det_ordered (1: detector planes 0-11 summed as 128-bit fixed-point integers, so identical
- * calls give identical bits; the packet-level moments stay floating-point sums)
+ * calls give identical bits; the packet-level moments stay floating-point sums), event_ldsu
+ * (0: k_event never stages its tables unpadded)
  * (transport.hip, TUNE).  Returns -22 for an unknown key or a value outside the key's range.
  * The production library reads no environment variable: the reference's drop-in never sees
  * a schedule it did not ask for.  The development build (libartes_hip_dev.so) also takes

@@ -1,5 +1,5 @@
 """Every k_event instantiation the engine's dispatch can pick (transport.hip, run_event_engine:
-`ev_v` 1-13) against the CPU oracle, trajectory by trajectory.
+`ev_v` 1-18) against the CPU oracle, trajectory by trajectory.
 
 The dispatch chooses from the call's shape: the scattering tables in LDS when the call's
 matrices fit (LDS_T; a uniform atmosphere's one matrix) or only their cumulative part
@@ -24,20 +24,28 @@ pytestmark = pytest.mark.gpu
 # (variant, atmosphere, detector, tuning, expected k_event template arguments)
 CASES = [
     (1, "uniform", "phase", {}, "1,0,1,768,0"),
-    (2, "cloudy", "phase", {}, "0,0,1,768,1"),
-    (3, "cloudy", "imaging", {}, "0,1,0,768,1"),
+    (2, "cloudy", "phase", dict(event_ldsu=0), "0,0,1,768,1"),
+    (3, "cloudy", "imaging", dict(event_ldsu=0), "0,1,0,768,1"),
     (4, "cloudy", "imaging", dict(det_lds=0), "0,0,0,768,1"),
-    (5, "cloudy", "phase", dict(event_ldsc=0), "0,0,1,768,0"),
+    (5, "cloudy", "phase", dict(event_ldsc=0, event_ldsu=0), "0,0,1,768,0"),
     (6, "uniform", "phase", dict(event_block=256), "1,0,1,256,0"),
     (7, "cloudy", "phase", dict(event_block=256), "0,0,1,256,0"),
     (8, "uniform", "imaging", {}, "1,1,0,768,0"),
     (9, "uniform", "imaging", dict(event_block=256), "1,1,0,256,0"),
     (10, "uniform", "imaging", dict(det_lds=0), "1,0,0,256,0"),
-    (11, "cloudy", "imaging", dict(event_ldsc=0), "0,1,0,768,0"),
+    (11, "cloudy", "imaging", dict(event_ldsc=0, event_ldsu=0), "0,1,0,768,0"),
     (12, "cloudy", "imaging", dict(event_block=256), "0,1,0,256,0"),
     (13, "cloudy", "imaging", dict(event_block=256, det_lds=0), "0,0,0,256,0"),
     (8, "uniform", "imaging", dict(msym=0), "1,1,0,768,0"),
     (3, "cloudy", "imaging", dict(msym=0), "0,1,0,768,1"),
+    # round 6: the fixed-point detector (det_ordered, ORD) and the unpadded LDS tables (TPAD = 0)
+    (14, "uniform", "imaging", dict(det_ordered=1), "1,0,0,768,0,2"),
+    (15, "cloudy", "phase", dict(det_ordered=1), "0,0,0,768,1,2"),
+    (16, "cloudy", "imaging", dict(det_ordered=1), "0,0,0,768,0,2"),
+    (17, "cloudy", "phase", {}, "1,0,1,768,0,0,0"),
+    (18, "cloudy", "imaging", {}, "1,1,0,768,0,0,0"),
+    (19, "cloudy", "imaging40", dict(det_ordered=1), "0,0,0,768,1,1"),
+    (20, "uniform", "imaging40", dict(det_ordered=1, event_ldsc=0), "0,0,0,768,0,1"),
 ]
 
 
@@ -59,6 +67,8 @@ def test_event_variant_matches_oracle(require_gpu, oracle_mod, atmospheres, case
     cfg = driver.default_config()
     if mode == "phase":
         cfg.apply("detector:type", "phase")
+    if mode == "imaging40":   # (a detector whose fixed-point planes exceed LDS: ORD = 1)
+        cfg.apply("detector:pixel", "40")
     det = driver.detector_geometry(cfg, float(atm["radial"][-1]))
     assert (det.nx == 1) == (mode == "phase")
     og = oracle_mod.OracleGrid(atm)
