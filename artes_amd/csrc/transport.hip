@@ -30,6 +30,13 @@
 
 #include "device_common.hpp"
 #include "kernel_persistent.hpp"
+
+// k_trace's step slots per loop iteration on fine 3D and radial-only grids (the coarse 3D grids'
+// 4: ARTES_COARSE_NREP): 10 since the fused radial step -- bench +1.1 %, ray3d / hg / iso k_trace
+// -1.3 / -2.1 / -1.2 % against 8; 9, 11 and 12 slower (profiles/r06/ab/trace_nrep_sweep_*.txt)
+#ifndef ARTES_FINE_NREP
+#define ARTES_FINE_NREP 10
+#endif
 #include "kernel_event.hpp"
 #include "kernel_trace.hpp"
 
@@ -135,7 +142,7 @@ struct TuneSpec {
 static const TuneSpec TUNE[T_NUM] = {
     {"engine", 0, 1},            // 0 the event engine, 1 the fused persistent engine (comparison tests)
     {"pool", 1024, 1LL << 26},   // packet-pool slots (default 131072 per CU)
-    {"steps", 4, 8},             // k_trace steps per loop iteration on 3D grids: 4 or 8
+    {"steps", 4, 16},            // k_trace steps per loop iteration on 3D grids: 4 or ARTES_FINE_NREP (10)
     {"refill", 1, 64},           // k_trace: refill a wave once this many lanes are idle
     {"static", 0, 64},           // statically dealt share of the trace list, in 1/64
     {"dgrab", 1, 4096},          // least list entries of a dynamic grab
@@ -246,7 +253,7 @@ static void tuning_from_env(artes_grid* g) {
         if (!e) continue;
         const long long v = k == T_ENGINE ? (std::string(e) == "persistent" ? 1 : 0) : atoll(e);
         g->tune[k] = std::max(TUNE[k].lo, std::min(TUNE[k].hi, v));
-        if (k == T_STEPS) g->tune[k] = v == 4 ? 4 : 8;
+        if (k == T_STEPS) g->tune[k] = v == 4 ? 4 : ARTES_FINE_NREP;
         if (k == T_EVENT_BLOCK) g->tune[k] = v == 256 ? 256 : 768;
     }
 }
@@ -323,11 +330,11 @@ int32_t artes_set_tuning(artes_grid* g, const char* key, int64_t value) {
     for (int k = 0; k < T_NUM; k++) {
         if (std::strcmp(key, TUNE[k].name) != 0) continue;
         if (value < 0) { g->tune[k] = -1; return 0; }   // back to the default
-        if (value < TUNE[k].lo || value > TUNE[k].hi || (k == T_STEPS && value != 4 && value != 8) ||
+        if (value < TUNE[k].lo || value > TUNE[k].hi || (k == T_STEPS && value != 4 && value != ARTES_FINE_NREP) ||
             (k == T_EVENT_BLOCK && value != 256 && value != 768))
             return fail(-22, std::string("tuning value out of range for ") + key);
-        if (k == T_STEPS && !(g->T.ntheta > 1 || g->T.nphi > 1) && value != 8)
-            return fail(-22, "steps: radial-only grids have the 8-step k_trace only");
+        if (k == T_STEPS && !(g->T.ntheta > 1 || g->T.nphi > 1) && value != ARTES_FINE_NREP)
+            return fail(-22, "steps: radial-only grids have the fine-grid k_trace only (" + std::to_string(ARTES_FINE_NREP) + " steps)");
         g->tune[k] = value;
         return 0;
     }
@@ -562,6 +569,7 @@ static int round_sub(int blocks) { return std::max(NSUB, (blocks + NSUB - 1) / N
 #ifndef ARTES_COARSE_NREP
 #define ARTES_COARSE_NREP 4
 #endif
+// (the default kernel on fine 3D and radial-only grids: ARTES_FINE_NREP, at the top of the file)
 template <bool G3D, bool OBL, int WPE, bool FLOW = false, int NREP = 8, bool GTAB = false>
 static void launch_trace(artes_grid* g, int bpc, const DevGrid& G, const DevRun& R, const SubLists& L, hipStream_t stream) {
     const size_t lds = GTAB ? 0 : trace_table_bytes(G.nr, G.ntheta, G.nphi);
@@ -598,7 +606,7 @@ static void launch_trace_tab(artes_grid* g, int wpe, int steps, int bpc, const D
     } else if (G3D && steps == 4) {
         launch_trace<G3D, false, 4, false, ARTES_COARSE_NREP, GTAB>(g, bpc, G, R, L, stream);
     } else {
-        launch_trace<G3D, false, 4, false, 8, GTAB>(g, bpc, G, R, L, stream);
+        launch_trace<G3D, false, 4, false, ARTES_FINE_NREP, GTAB>(g, bpc, G, R, L, stream);
     }
 }
 template <bool G3D>
@@ -658,7 +666,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     // 3D and radial-only grids, 4 on coarse 3D grids (< 4096 cells), whose short chains leave
     // more lanes idle for the rest of an iteration (profiles/r04/ab/trace_nrep*_ab.txt);
     // tuning "steps" = 4 | 8 overrides (3D grids; the oblate, flow and wpe = 3 kernels have 8)
-    const int trace_steps = (int)tv(g, T_STEPS, G.ncell < 4096 ? 4 : 8);
+    const int trace_steps = (int)tv(g, T_STEPS, G.ncell < 4096 ? 4 : ARTES_FINE_NREP);
     // k_trace's face tables: in LDS up to 64 KiB (two blocks per CU at most then), beyond that
     // in global memory (GTAB kernels, L2-resident: ~2000 radial faces and more); tuning
     // "trace_gtab" = 1 forces the global tables (tests)

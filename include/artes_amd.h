@@ -245,7 +245,7 @@ int32_t artes_run_trace(artes_grid* grid, const artes_run_params* params,
  * optimum).  No key except "engine" changes a per-packet result: they move the schedule only.
  * Keys: engine (0 event engine, 1 the fused persistent engine), pool (slots; a pool larger than
  * the setting is reallocated at the next call), steps (k_trace
- * steps per iteration, 4 or 8, 3D grids), refill, static, dgrab, batch, batch_min, hbatch,
+ * steps per iteration, 4 or 10, 3D grids), refill, static, dgrab, batch, batch_min, hbatch,
  * gbatch, defer, backward, emit_first, late_append, pix1, det_lds, event_lds, event_ldsc,
  * event_block (256 or 768), event_bpc, trace_bpc, wpe (3 or 4), msym, max_it, verbose,
  * trace_gtab (k_trace's face tables in global memory; automatic when they exceed 64 KiB),

@@ -67,7 +67,7 @@ def test_pool_key_shrinks_an_existing_pool_and_last_launch_names_the_engine(requ
     assert len(pools) == 2 and pools[0] > 5000 >= pools[1] - 1023, err
     np.testing.assert_array_equal(base.counters, other.counters)
     np.testing.assert_allclose(base.det, other.det, rtol=1e-9, atol=1e-300)
-    assert grid.last_launch().startswith("k_trace<0,0,4,0,8>")
+    assert grid.last_launch().startswith("k_trace<0,0,4,0,10>")
     grid.run(p, 0, 0, 99)
     assert grid.last_launch() == "none"
 
@@ -205,11 +205,12 @@ def test_bench_line_contract(require_gpu):
 
 def test_tuning_keys_are_checked(require_gpu):
     """artes_set_tuning: unknown keys and out-of-range values fail with -22 ("steps"
-    other than 4 / 8 used to map silently to 8); -1 restores a default."""
+    other than 4 / 8 used to map silently to 8; the fine-grid kernel has 10 steps since round 6); -1
+    restores a default."""
     from artes_amd.engine import EngineError
 
     atm, grid, p = _setup(nr=8, ntheta=8, nphi=8)
-    for bad in (dict(steps=2), dict(steps=6), dict(batch_min=0), dict(event_block=512), dict(wpe=5), dict(nosuchkey=1)):
+    for bad in (dict(steps=2), dict(steps=6), dict(steps=8), dict(batch_min=0), dict(event_block=512), dict(wpe=5), dict(nosuchkey=1)):
         with pytest.raises(EngineError):
             grid.set_tuning(**bad)
     assert grid.tuning() == {}
@@ -256,4 +257,4 @@ def test_production_library_ignores_environment(require_gpu):
     d0, d1 = outs[0].pop("d"), outs[1].pop("d")
     assert abs(d0 - d1) <= 1e-12 * abs(d0)
     assert outs[0] == outs[1]
-    assert outs[0]["l"] == "k_trace<1,0,4,0,8> k_event<1,1,0,768,0>" and outs[0]["t"] == {}
+    assert outs[0]["l"] == "k_trace<1,0,4,0,10> k_event<1,1,0,768,0>" and outs[0]["t"] == {}

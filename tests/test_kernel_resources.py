@@ -64,12 +64,15 @@ def test_k_trace_budgets():
 
 
 def test_k_trace_step_counts():
-    # steps per loop iteration: 8 on fine 3D and radial-only grids, 4 on coarse
-    # 3D grids -- both 3D instantiations and the radial-only one with 8 must be in the library
+    # steps per loop iteration: 10 on fine 3D and radial-only grids (8 before
+    # round 6), 4 on coarse 3D grids -- both 3D instantiations and the radial-only one with 10 must
+    # be in the library, with their global-table (GTAB) twins
     ks = _kernels()
-    _find(ks, "_ZN5artes7k_traceILb1ELb0ELi4ELb0ELi8E")
-    _find(ks, "_ZN5artes7k_traceILb1ELb0ELi4ELb0ELi4E")
-    _find(ks, "_ZN5artes7k_traceILb0ELb0ELi4ELb0ELi8E")
+    _find(ks, "_ZN5artes7k_traceILb1ELb0ELi4ELb0ELi10ELb0E")
+    _find(ks, "_ZN5artes7k_traceILb1ELb0ELi4ELb0ELi4ELb0E")
+    _find(ks, "_ZN5artes7k_traceILb0ELb0ELi4ELb0ELi10ELb0E")
+    _find(ks, "_ZN5artes7k_traceILb1ELb0ELi4ELb0ELi10ELb1E")
+    _find(ks, "_ZN5artes7k_traceILb0ELb0ELi4ELb0ELi10ELb1E")
 
 
 def test_k_event_and_k_emit_budgets():
