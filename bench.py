@@ -113,8 +113,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the untimed parity step (profiling passes)")
     ap.add_argument("--no-variants", action="store_true", help="skip the untimed configs[2] (32x16x32) leg (profiling passes)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05", "pmc_summary.json"))
-    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r05", "pmc_sq_summary.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r06", "pmc_summary.json"))
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "r06", "pmc_sq_summary.json"))
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="an artes_set_tuning override of the bench grid (measurements only, e.g. det_ordered=1; "
                          "reported under engine.tuning)")
