@@ -1345,10 +1345,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     const int kn = tcr + (side ? 1 : -1);
                     const double2 rrn = T.rr[kn];
                     const int nfi = side ? kn : tcr;
-                    const bool runaway = ncross >= nlim;
-                    const bool exit = side & (nfi == G.nr) & !runaway;
-                    const bool surf = (nfi == G.cell_depth) & !runaway;
-                    bool err = runaway | ((tft == 1) & (tfi == G.cell_depth) & surf);
+                    // (a runaway trace -- 2^22 crossings -- is stopped at the end of the iteration, below)
+                    const bool exit = side & (nfi == G.nr);
+                    const bool surf = nfi == G.cell_depth;
+                    bool err = (tft == 1) & (tfi == G.cell_depth) & surf;
     #ifdef ARTES_DEBUG
                     if (!err && !exit && !surf && (kn < 0 || kn >= G.nr)) {   // (ARTES_ERR_CELL, as below)
                         log_err(R, ARTES_ERR_CELL);
@@ -1367,8 +1367,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     if (!hitpark) {
                         tacc += tau_cell;
                         tpar = e0;
-                        tft = 1; tfi = nfi;
                     }
+                    // (the face also for a lane whose interaction lies in this cell: interaction()
+                    // resets it before the peel-off, and an absorbed packet's face is dead)
+                    tft = 1; tfi = nfi;
                     if (!stop) {
                         cell += kn - tcr;
                         tcr = kn;
@@ -1569,16 +1571,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             // every lane that stopped in any of them, once per iteration.  (A surface's albedo draw
             // moves here from the step: the lane draws nothing in between, so its RNG sequence is
             // unchanged.)
+            // (the radial-form steps leave the runaway test to here, once per iteration: a trace still
+            // stepping past nlim crossings ends as the generic step's runaway does)
+            if (have && !parked && !end && ncross >= nlim) parked = PK_END | PK_ERR31 | PK_RUNAWAY | PK_ERR;
             if (__ballot(parked >= PK_END)) {
                 if (parked >= PK_END) {
                     int sk = parked;
                     parked = 0;
                     if (sk & PK_RAD) {
                         // the radial-form step (ARTES.f90:2885-3010 faces): the packet crossed sphere tfi
-                        // (tft = 1); a runaway is the crossing count past nlim (it was counted), exit the
-                        // top sphere and the surface sphere cell_depth otherwise
-                        const bool runaway = (sk & PK_ERR) && ncross > nlim;
-                        sk |= runaway ? (PK_ERR31 | PK_RUNAWAY) : ((tfi == G.nr ? PK_EXIT : 0) | (tfi == G.cell_depth ? PK_SURF : 0));
+                        // (tft = 1): the top sphere is the exit, sphere cell_depth the surface
+                        sk |= (tfi == G.nr ? PK_EXIT : 0) | (tfi == G.cell_depth ? PK_SURF : 0);
                     }
                     const bool exit = (sk & PK_EXIT) != 0, surf = (sk & PK_SURF) != 0, err = (sk & PK_ERR) != 0;
                     if (err) {
