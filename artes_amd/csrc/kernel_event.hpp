@@ -1117,8 +1117,13 @@ __device__ __forceinline__ void wave_store_lines(const uint4* st, void* dst) {
     __builtin_amdgcn_wave_barrier();
 }
 
-template <bool G3D, bool TRACE>
-__global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, SubLists SL) {
+// STAR: the star source alone (photon:source=star) -- no thermal emission, no flux sums -- so the
+// planet branch's registers do not set the kernel's budget: 106 VGPRs on 3D grids (159 with the
+// branch), 4 waves per SIMD instead of 3 (the LDS line stage allows 4 blocks per CU).  k_emit
+// waits on memory; the 4th wave hides more of it: bench k_emit 38.9 -> 34.3 ms per step
+// (profiles/r06/ab/emit_star_waves_ab.txt; radial-only grids: 98 VGPRs either way, no hint)
+template <bool G3D, bool TRACE, bool STAR = false>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu((STAR && G3D) ? 4 : 1))) void k_emit(DevGrid G, DevRun R, Pool S, SubLists SL) {
     const Lists L = SL.l[sub_of_block()];
     extern __shared__ double s_em[];
     __shared__ uint4 s_lines[BLOCK / 64 * LINE_STAGE];
@@ -1181,7 +1186,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
                 const double a0 = S.d[slot].pt0, a1 = S.d[slot].pt1, a2 = S.d[slot].pt2, a3 = S.d[slot].pt3;
                 t2[0] += a0 * a0; t2[1] += a1 * a1; t2[2] += a2 * a2; t2[3] += a3 * a3;
             }
-            if (m == S_END_EXIT && R.photon_source == 2) f_exit += S.s[slot].wI;
+            if (!STAR && m == S_END_EXIT && R.photon_source == 2) f_exit += S.s[slot].wI;
             if constexpr (TRACE) {
                 double* rr = R.rec + (size_t)(S.d[slot].pid - R.first) * ARTES_TRACE_FIELDS;
                 rr[0] = S.d[slot].peel_sum;
@@ -1206,7 +1211,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
         rng.seed(R.seed, pid);
         double px, py, pz, dx, dy, dz, wI = 1.0;
         int cr = G.nr - 1, ct = 0, cp = 0, face = pack_face(1, G.nr), mode0 = S_FIRST;
-        if (R.photon_source == 2) {
+        if (!STAR && R.photon_source == 2) {
             double bias;
             emit_planet(G, R, rng, px, py, pz, dx, dy, dz, cr, ct, cp, bias);
             // weight for the cell emission probability (ARTES.f90:605), then peel_thermal
@@ -1300,7 +1305,7 @@ __global__ __launch_bounds__(BLOCK) void k_emit(DevGrid G, DevRun R, Pool S, Sub
         if (q2 != 0.0) tot_add(R, 2, q2);
         if (q3 != 0.0) tot_add(R, 3, q3);
     }
-    if (R.photon_source == 2) {
+    if (!STAR && R.photon_source == 2) {
         const double fe = wave_sum_f64(f_emit), fx = wave_sum_f64(f_exit);
         if ((threadIdx.x & 63) == 0) {
             if (fe != 0.0) tot_add(R, 4, fe);

@@ -758,7 +758,9 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     };
     const size_t em_lds = G3D ? emit_table_doubles(G.ntheta, G.nphi) * sizeof(double) : 0;
     auto launch_emit = [&](const SubLists& L) {
+        const bool star = R.photon_source != 2;
         if (trace) hipLaunchKernelGGL((k_emit<G3D, true>), dim3(side_blocks), dim3(BLOCK), em_lds, stream, G, R, g->pool, L);
+        else if (star) hipLaunchKernelGGL((k_emit<G3D, false, true>), dim3(side_blocks), dim3(BLOCK), em_lds, stream, G, R, g->pool, L);
         else hipLaunchKernelGGL((k_emit<G3D, false>), dim3(side_blocks), dim3(BLOCK), em_lds, stream, G, R, g->pool, L);
     };
     SubUse use;

@@ -83,3 +83,6 @@ def test_k_event_and_k_emit_budgets():
             assert r["vgpr_count"] <= 170, (name, r)
     for name, r in _find(ks, "_ZN5artes6k_emit").items():
         assert r["vgpr_spill_count"] == 0, (name, r)
+    # the star-source emission on 3D grids: 4 waves per SIMD (kernel_event.hpp, STAR)
+    for name, r in _find(ks, "_ZN5artes6k_emitILb1ELb0ELb1E").items():
+        assert r["vgpr_count"] <= 128, (name, r)
