@@ -232,12 +232,24 @@ __device__ __forceinline__ double min_nonan(double a, double b) {
 
 constexpr double INF = __builtin_inf();
 
+// k_trace's face the packet sits on, as one code: (type - 1) << 16 | index for a radial (type 1),
+// theta (2) or phi (3) face -- a radial face's code is its index -- and -1 for none (type 0).
+// One register instead of two, and "on sphere k" is one compare (the record keeps pack_face's
+// form; the event engine's cell packing keeps every index <= 4096, transport.hip)
+__device__ __forceinline__ int face_code(int type, int idx) { return type == 0 ? -1 : ((type - 1) << 16) | idx; }
+__device__ __forceinline__ int face_code_type(int tf) { return (tf >> 16) + 1; }   // (arithmetic shift: -1 -> 0)
+__device__ __forceinline__ int face_code_index(int tf) { return tf < 0 ? 0 : (tf & 0xFFFF); }
+
 // k_trace's `parked` codes: 1 (3 after a cell error) the forced first interaction waits, 4 the
 // interaction waits; PK_END and its bits (trace-relative kernels): a trace end found in a step,
 // resolved at the end of the iteration
 // PK_RAD: a trace end of the radial-form step, whose exit / surface / runaway bits the end block
-// derives from the state (tfi the sphere crossed, ncross against nlim) instead of the step
-enum : int { PK_END = 8, PK_EXIT = 16, PK_SURF = 32, PK_ERR31 = 64, PK_RUNAWAY = 128, PK_ERR = 256, PK_RAD = 512 };
+// derives from the state (tf the sphere crossed, ncross against nlim) instead of the step; its
+// codes PK_RAD_END and PK_RAD_ERR are inline constants of the instruction set (<= 64), so the step
+// selects them with no literal moves (bits 0-1 of a code >= PK_END are free: the parked-lane
+// tests of the loop head see codes 1, 3, 4 only)
+enum : int { PK_END = 8, PK_EXIT = 16, PK_SURF = 32, PK_ERR31 = 64, PK_RUNAWAY = 128, PK_ERR = 256, PK_RAD = 1, PK_RAD_E = 2 };
+enum : int { PK_RAD_END = PK_END | PK_RAD, PK_RAD_ERR = PK_END | PK_RAD | PK_RAD_E };
 // a new trace's set-up (k_trace's common set-up block): the start cell from the packet position,
 // the direction's constants
 enum : int { NT_POS = 1, NT_DIR = 2 };
@@ -279,7 +291,7 @@ __device__ __forceinline__ double dir_axy(double ax2, double by2, double d0, dou
 // monotone AND/OR of comparisons (no selects of booleans), which stay lane masks.
 template <bool G3D, bool OBL>
 __device__ __forceinline__ double family_eval(const DevGrid& G, const TraceTabs& T, int fam, double x, double y, double z,
-                                              double n0, double n1, double n2, double Axy, double Az, int ft, int fi,
+                                              double n0, double n1, double n2, double Axy, double Az, int tf,
                                               int cr, int ct, int cp, int pout, double zp, bool& outer) {
     const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
     [[maybe_unused]] const bool isR = !G3D || fam == 0;
@@ -316,8 +328,8 @@ __device__ __forceinline__ double family_eval(const DevGrid& G, const TraceTabs&
     const double b1 = fast_div(qc1, q1);
     const int kout = kin + 1;
     const int kin_f = isP ? cp : kin, kout_f = isP ? pout : kout;
-    const bool onfam = ft == fam + 1;
-    const bool same0 = onfam & (fi == kin_f), same1 = onfam & (fi == kout_f);
+    const int fb = fam << 16;   // (the face code, see face_code)
+    const bool same0 = tf == kin_f + fb, same1 = tf == kout_f + fb;
     const bool plane0 = G3D && (fin.flags & FR_PL), plane1 = G3D && (fout.flags & FR_PL);   // (theta lanes only)
     // existence: the divisor, and for the quadratic the discriminant
     const bool d_ok0 = isP | (disc0 >= 0.0), d_ok1 = isP | (disc1 >= 0.0);
@@ -385,7 +397,7 @@ __device__ __forceinline__ double family_eval(const DevGrid& G, const TraceTabs&
 // here: the sphere's face choice folds away.
 template <bool G3D, bool OBL, bool NORAD = false>
 __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs& T, int fam, double x, double y, double z,
-                                               double n0, double n1, double n2, double Axy, double Az, int ft, int fi,
+                                               double n0, double n1, double n2, double Axy, double Az, int tf,
                                                int cr, int ct, int cp, int pout, double zp, bool alt, const TraceK& K,
                                                bool& outer) {
     const double ax2 = OBL ? G.ax2 : 1.0, by2 = OBL ? G.by2 : 1.0, cz2 = OBL ? G.cz2 : 1.0;
@@ -395,8 +407,8 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     const double Cxy = ax2 * x * x + by2 * y * y, Cz = cz2 * z * z;
     const int kin = isT ? ct : cr;
     const int e = (isT ? G.nr + 1 : 0) + kin;
-    const bool onfam = ft == fam + 1;
-    const bool same_in = onfam & (fi == (isP ? cp : kin));
+    const int fb = fam << 16;   // (the face code, see face_code)
+    const bool same_in = tf == (isP ? cp : kin) + fb;
     // which face: the sphere rule needs the inner face's discriminant (w = 1)
     bool ch;
     if constexpr (NORAD) {   // theta: the face theta moves to; phi: (unused)
@@ -435,7 +447,7 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
     const double rA = fast_div(isP ? num0 : q, dA);
     const double rB = fast_div(isP ? num1 : qc, dB);
     const int kA = isP ? cp : kin + (ch ? 1 : 0), kB = isP ? pout : kA;
-    const bool sameA = onfam & (fi == kA), sameB = onfam & (fi == kB);
+    const bool sameA = tf == kA + fb, sameB = tf == kB + fb;
     // existence: the divisor, and for the quadratic the discriminant
     const bool d_ok = isP | (disc >= 0.0);
     bool vA = d_ok & (fabs(dA) > K.tiny);
@@ -491,13 +503,11 @@ __device__ __forceinline__ double family_eval1(const DevGrid& G, const TraceTabs
 // is vetoed as the inner face, 1e-15 m otherwise, equal roots and >= 1e100 give none.
 // Returns the crossing's trace parameter s (a NaN: none).  The roots differ from the
 // reference's per-step re-solve by rounding (~1e-8 m at 7e7 m); the trajectory tests bound it.
-__device__ __forceinline__ double radial_tr(const TraceTabs& T, double b0, double pm, double t, int ft, int fi, int cr,
+__device__ __forceinline__ double radial_tr(const TraceTabs& T, double b0, double pm, double t, int tf, int cr,
                                             bool alt, const TraceK& K, bool& outer) {
     const double2 rr = T.rr[cr];
-    const bool onr = ft == 1;
-    // the packet sits on the shell's inner / outer sphere
-    const int df = fi - cr;
-    const bool s_in = onr & (df == 0), s_out = onr & (df == 1);
+    // the packet sits on the shell's inner / outer sphere (a radial face's code is its index)
+    const bool s_in = tf == cr, s_out = tf == cr + 1;
     const bool in_ok = (t < -b0) & (rr.x >= pm) & !s_in;
     const bool ch = in_ok == alt;   // outer face: !in_ok, turned by alt
     const double r = ch ? rr.y : rr.x;
@@ -554,15 +564,14 @@ __device__ __forceinline__ double radial_next(const double2 rr, double b0, doubl
 // linear in the trace parameter, so from the trace's start; family_eval1's rules for phi with
 // the distances from the current point s - t (the half-plane the packet sits on, and the sp0
 // quirk: the outer face vetoed when the inner one's root is >= 1e100, 3318, 3346).
-__device__ __forceinline__ double phi_tr(const TraceTabs& T, double x0, double y0, double n0, double n1, double t, int ft, int fi,
+__device__ __forceinline__ double phi_tr(const TraceTabs& T, double x0, double y0, double n0, double n1, double t, int tf,
                                          int cp, int pout, const TraceK& K, bool& outer) {
     const double2 sc0 = T.phsc[cp], sc1 = T.phsc[pout];
     const double den0 = n1 * sc0.y - n0 * sc0.x, num0 = x0 * sc0.x - y0 * sc0.y;
     const double den1 = n1 * sc1.y - n0 * sc1.x, num1 = x0 * sc1.x - y0 * sc1.y;
     const double sA = fast_div(num0, den0), sB = fast_div(num1, den1);
     const double dA = sA - t, dB = sB - t;
-    const bool onp = ft == 3;
-    const bool sameA = onp & (fi == cp), sameB = onp & (fi == pout);
+    const bool sameA = tf == cp + (2 << 16), sameB = tf == pout + (2 << 16);   // (phi face codes, face_code)
     const bool sp0_big = !sameA & (fabs(den0) > 0.0) & !(dA < K.huge);
     const bool vA = (fabs(den0) > K.tiny) & (dA > K.tol) & !sameA & (dA < K.huge);
     const bool vB = (fabs(den1) > K.tiny) & (dB > K.tol) & !(sameB | sp0_big) & (dB < K.huge);
@@ -677,7 +686,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     int slot = -1, mode = 0, pcell = 0, pface = 0, ncross = 0;
     double px = 0, py = 0, pz = 0, ttgt = 0, wI = 0;
     Rng rng{0, 0};
-    int tcr = 0, tct = 0, tcp = 0, tft = 0, tfi = 0, pending = 0, cell = 0;
+    int tcr = 0, tct = 0, tcp = 0, tf = -1, pending = 0, cell = 0;   // tf: face_code
     double tx = 0, ty = 0, tz = 0, nx = 0, ny = 0, nz = 0, tacc = 0, inz = 0, Axy = 0, Az = 0;
     // extinction and albedo weight of the current cell, loaded when the cell changes: the L2 round
     // trip overlaps the next iteration's face evaluation (one 16-byte load at a 32-bit byte
@@ -803,7 +812,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     auto start_position = [&]() {
         tx = px; ty = py; tz = pz;
         unpack_cell(pcell, tcr, tct, tcp);
-        unpack_face(pface, tft, tfi);
+        {
+            int ft, fi;
+            unpack_face(pface, ft, fi);
+            tf = face_code(ft, fi);
+        }
 #ifdef ARTES_DEBUG
         if (tcr >= G.nr || tct >= G.ntheta || tcp >= G.nphi) {   // (ARTES_ERR_CELL: the run fails; no out-of-range read)
             log_err(R, ARTES_ERR_CELL);
@@ -830,7 +843,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         // The propagation that follows walks the first trace's chord again, from its start
         // to optical depth tau (ARTES.f90:689-720).  When the interaction lies in the
         // chord's far half it is reached in fewer cells from the far end: walk back from
-        // where the first trace stopped (tx, tft, tfi, cell: set when the lane parked) to
+        // where the first trace stopped (tx, tf, cell: set when the lane parked) to
         // optical depth tau_first - tau.  Same cells in reverse, so the same interaction
         // point up to rounding; crossing counts are kept as the forward walk's (kb).  Not
         // with the flow diagnostics (segment order).
@@ -865,7 +878,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
             if (S2 < G.rf2[tcr] * (1 - 1e-9) || S2 > G.rf2[tcr + 1] * (1 + 1e-9)) {
                 if (atomicAdd(&R.err[ARTES_ERR_GEOM], 1ULL) < 6)
                     printf("[geom] hit outside shell: t %.17g %.17g %.17g n %.17g %.17g %.17g cell %d %d %d face %d %d e %.17g %.17g %.17g sides %x s %.17g steps left %d mode %d S2/rf2 %.17g %.17g\n",
-                           tx, ty, tz, nx, ny, nz, tcr, tct, tcp, tft, tfi, e0, e1, e2, sides, s, nlim - ncross, mode,
+                           tx, ty, tz, nx, ny, nz, tcr, tct, tcp, face_code_type(tf), face_code_index(tf), e0, e1, e2, sides, s, nlim - ncross, mode,
                            S2 / G.rf2[tcr], S2 / G.rf2[tcr + 1]);
             }
         }
@@ -892,7 +905,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         c_peel++;
         mode = S_PEEL;
         tx = px; ty = py; tz = pz;
-        tft = 0; tfi = 0;
+        tf = -1;
         nx = R.det0; ny = R.det1; nz = R.det2;
         if constexpr (SETUP_MERGED) nt = NT_DIR;   // (the set-up: the iteration's common block, below)
         else set_direction(nx, ny, nz);
@@ -1153,7 +1166,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 if (pending & 1) {
                     const bool alt = (sides >> 4) & 1;
                     bool outer;
-                    const double dm = radial_tr(T, b0, pm, tpar, tft, tfi, tcr, alt, K, outer);
+                    const double dm = radial_tr(T, b0, pm, tpar, tf, tcr, alt, K, outer);
                     const bool retry = !alt & !(dm < K.inf);
                     // (the other face is still to come: the entry is the current trace parameter,
                     // the nearest one, and the bit stays pending)
@@ -1223,12 +1236,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                             bool outer;
                             double dm;
                             if (fam == 2) {
-                                dm = phi_tr(T, tx, ty, nx, ny, tpar, tft, tfi, tcp, pout, K, outer);
+                                dm = phi_tr(T, tx, ty, nx, ny, tpar, tf, tcp, pout, K, outer);
                             } else {   // theta (~0.1-0.4 % of crossings): from the current point
                                 TM_TICK(ta);
                                 const double qx = fma(tpar, nx, tx), qy = fma(tpar, ny, ty), qz = fma(tpar, nz, tz);
                                 dm = tpar + family_eval1<G3D, OBL, true>(G, T, fam, qx, qy, qz, nx, ny, nz, dir_axy(ax2, by2, nx, ny),
-                                                                         cz2 * nz * nz, tft, tfi, tcr, tct, tcp, pout, -qz * fast_rcp(nz),
+                                                                         cz2 * nz * nz, tf, tcr, tct, tcp, pout, -qz * fast_rcp(nz),
                                                                          alt, K, outer);
                                 TM_TICK(tb);
                                 TM_ADD(5, tb - ta);
@@ -1281,10 +1294,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                 double dm;
                 bool retry = false;
                 if constexpr (OBL || TWOFACE) {
-                    dm = family_eval<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, outer);
+                    dm = family_eval<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tf, tcr, tct, tcp, pout, -tz * inz, outer);
                 } else {
                     const bool alt = (sides >> (4 + fam)) & 1;
-                    dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tft, tfi, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
+                    dm = family_eval1<G3D, OBL>(G, T, fam, tx, ty, tz, nx, ny, nz, Axy, Az, tf, tcr, tct, tcp, pout, -tz * inz, alt, K, outer);
                     retry = (fam != 2) & !alt & !(dm < K.inf);
                 }
                 // (the other face is still to come: no bound.  Only the high word is cleared: the
@@ -1342,13 +1355,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     // The new shell's radii are read before the trace-end tests (rr[kn] for
                     // kn = -1 .. nr: padded, used only when the packet stays in the grid).
                     const bool side = sides & 1;
-                    const int kn = tcr + (side ? 1 : -1);
+                    const int dk = side ? 1 : -1;
+                    // (kn out of the compiler's sight: the new shell's index for the radii read and the
+                    // face, while tcr moves in place below -- as one value the two branches' tcr met in
+                    // two copies at the join)
+                    int kn;
+                    asm("v_add_u32 %0, %1, %2" : "=v"(kn) : "v"(tcr), "v"(dk));
                     const double2 rrn = T.rr[kn];
                     const int nfi = side ? kn : tcr;
                     // (a runaway trace -- 2^22 crossings -- is stopped at the end of the iteration, below)
                     const bool exit = side & (nfi == G.nr);
                     const bool surf = nfi == G.cell_depth;
-                    bool err = (tft == 1) & (tfi == G.cell_depth) & surf;
+                    bool err = (tf == G.cell_depth) & surf;
     #ifdef ARTES_DEBUG
                     if (!err && !exit && !surf && (kn < 0 || kn >= G.nr)) {   // (ARTES_ERR_CELL, as below)
                         log_err(R, ARTES_ERR_CELL);
@@ -1370,10 +1388,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     }
                     // (the face also for a lane whose interaction lies in this cell: interaction()
                     // resets it before the peel-off, and an absorbed packet's face is dead)
-                    tft = 1; tfi = nfi;
+                    tf = nfi;
                     if (!stop) {
-                        cell += kn - tcr;
-                        tcr = kn;
+                        cell += dk;
+                        tcr += dk;
                         load_cell();
                         bool outer;
                         const double dm = radial_next(rrn, b0, pm, tpar, side, K, outer);
@@ -1382,7 +1400,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         pending |= (dm < K.inf) ? 0 : 1;   // (NaN: radial_tr in the next slot, alt)
                     } else {
                         // (the end's reasons follow from the state at the end of the iteration: PK_RAD)
-                        parked = hitpark ? 4 : (PK_END | PK_RAD | (err ? PK_ERR : 0));
+                        parked = hitpark ? 4 : (err ? PK_RAD_ERR : PK_RAD_END);
                     }
                 }   // rstep
             } else if (do_step) {
@@ -1425,7 +1443,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     const bool err31 = !(best < K.inf) | runaway;
                     const bool exit = (w == 0) & side & (nfi == G.nr) & !err31;
                     const bool surf = (w == 0) & (nfi == G.cell_depth) & !err31;
-                    bool err = err31 | ((tft == 1) & (tfi == G.cell_depth) & surf);
+                    bool err = err31 | ((tf == G.cell_depth) & surf);
         #ifdef ARTES_DEBUG
                     {   // the new index of the crossed family must name a cell unless the trace leaves
                         // the grid or reaches the surface (ARTES_ERR_CELL: the packet is dropped before
@@ -1466,7 +1484,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         if (!hitpark) {
                             tacc += tau_cell;
                             tpar = best_abs;
-                            tft = w + 1; tfi = nfi;
+                            tf = nfi | (w << 16);
                         }
                         if (!stop) {
                             if constexpr (G3D) {
@@ -1495,7 +1513,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                             } else {
                                 tx = fma(best, nx, tx); ty = fma(best, ny, ty); tz = fma(best, nz, tz);
                             }
-                            tft = w + 1; tfi = nfi;
+                            tf = nfi | (w << 16);
                             if constexpr (G3D) {
                                 tcr = w == 0 ? kn : tcr;
                                 tct = w == 1 ? kn : tct;
@@ -1555,7 +1573,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                                 // until enough lanes of the wave need it (see the top of the loop)
                                 const double sf = TREL ? best_abs : best;
                                 tx += sf * nx; ty += sf * ny; tz += sf * nz;
-                                tft = w + 1; tfi = nfi;
+                                tf = nfi | (w << 16);
                                 parked = err ? 3 : 1;
                             }
                         }
@@ -1579,9 +1597,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     int sk = parked;
                     parked = 0;
                     if (sk & PK_RAD) {
-                        // the radial-form step (ARTES.f90:2885-3010 faces): the packet crossed sphere tfi
-                        // (tft = 1): the top sphere is the exit, sphere cell_depth the surface
-                        sk |= (tfi == G.nr ? PK_EXIT : 0) | (tfi == G.cell_depth ? PK_SURF : 0);
+                        // the radial-form step (ARTES.f90:2885-3010 faces): the packet crossed sphere tf
+                        // (a radial face code): the top sphere is the exit, sphere cell_depth the surface
+                        sk |= (tf == G.nr ? PK_EXIT : 0) | (tf == G.cell_depth ? PK_SURF : 0) | ((sk & PK_RAD_E) ? PK_ERR : 0);
                     }
                     const bool exit = (sk & PK_EXIT) != 0, surf = (sk & PK_SURF) != 0, err = (sk & PK_ERR) != 0;
                     if (err) {
