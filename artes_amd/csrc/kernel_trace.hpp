@@ -707,6 +707,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     // side (bit f of `sides`: 0 inner, 1 outer face)
     double e0 = INF, e1 = INF, e2 = INF;
     int sides = 0;
+    // the radial family's side as the step direction of the shell index (+1: the outer sphere is
+    // next, -1: the inner one), apart from `sides` (whose bit 0 the radial family then leaves
+    // unused): the fused step adds it to the index as it is, and the evaluation writes it with one
+    // select -- the bit's extraction, test and select and its insertion were five instructions
+    int rdk = -1;
     // crossings: counted per packet (ncross, in the record) and added to the lane's total
     // once per chain, from the chain's start value nc0 (not per step)
     uint32_t c_cross = 0, c_peel = 0;
@@ -804,6 +809,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
         nlim = ncross + (1 << 22);
         pending = fam_all;
         sides = 0;
+        rdk = -1;
         set_bounds();
         if constexpr (G3D && !TREL) inz = fast_rcp(nz);
         set_trel();
@@ -1171,7 +1177,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     // (the other face is still to come: the entry is the current trace parameter,
                     // the nearest one, and the bit stays pending)
                     e0 = retry ? tpar : dm;
-                    sides = (sides & ~0x11) | (outer ? 1 : 0) | (retry ? 16 : 0);
+                    sides = (sides & ~0x10) | (retry ? 16 : 0);
+                    rdk = outer ? 1 : -1;
                     clear_pending(0, retry);
 #ifdef ARTES_DEBUG_LANES
                     dbg_r = retry; dbg_u = true;
@@ -1309,9 +1316,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     e1 = fam == 1 ? dm : e1;
                     e2 = fam == 2 ? dm : e2;
                     sides = (sides & ~(0x11 << fam)) | (((outer ? 1 : 0) | (retry ? 16 : 0)) << fam);
+                    rdk = fam == 0 ? (outer ? 1 : -1) : rdk;
                 } else {
                     e0 = dm;
                     sides = (outer ? 1 : 0) | ((retry ? 1 : 0) << 4);
+                    rdk = outer ? 1 : -1;
                 }
                 // the evaluated family's entry is exact now: clear ITS bit (see clear_pending)
                 clear_pending(fam, retry);
@@ -1354,8 +1363,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     // on the sphere it just crossed), so the lane's next slot needs no evaluation.
                     // The new shell's radii are read before the trace-end tests (rr[kn] for
                     // kn = -1 .. nr: padded, used only when the packet stays in the grid).
-                    const bool side = sides & 1;
-                    const int dk = side ? 1 : -1;
+                    const int dk = rdk;
+                    const bool side = dk > 0;
                     // (kn out of the compiler's sight: the new shell's index for the radii read and the
                     // face, while tcr moves in place below -- as one value the two branches' tcr met in
                     // two copies at the join)
@@ -1396,7 +1405,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                         bool outer;
                         const double dm = radial_next(rrn, b0, pm, tpar, side, K, outer);
                         e0 = dm;
-                        sides = (sides & ~1) | (outer ? 1 : 0);
+                        rdk = outer ? 1 : -1;
                         pending |= (dm < K.inf) ? 0 : 1;   // (NaN: radial_tr in the next slot, alt)
                     } else {
                         // (the end's reasons follow from the state at the end of the iteration: PK_RAD)
@@ -1428,7 +1437,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
                     // next_cell (ARTES.f90:2671-2798): the crossed family's index moves by one
                     // (phi wraps); the face index is the old one (inner face) or the new one
                     // (outer face) for every family
-                    const bool side = (sides >> w) & 1;
+                    const bool side = w == 0 ? rdk > 0 : ((sides >> w) & 1);
                     const int kf = !G3D ? tcr : (w == 0 ? tcr : (w == 1 ? tct : tcp));
                     int kn = kf + (side ? 1 : -1);
                     if constexpr (G3D) {   // (branch-free: a divergent branch costs more scalar work)
