@@ -237,7 +237,12 @@ struct artes_grid {
     bool prof = false;
     std::vector<hipEvent_t> prof_ev;     // start/end pairs
     std::vector<int> prof_kind;
+    std::vector<int> prof_start;         // per launch: the index in prof_ev of its start event
     size_t prof_used = 0;
+    // inside the engine's iteration loop the launches follow each other on the stream with nothing
+    // in between (until the live-count poll), so a launch starts at the previous launch's end event:
+    // one event per launch instead of two (the bench's profiled step: 904 -> 899 ms with none at all)
+    bool prof_loop = false, prof_chain = false;
 };
 
 // a tuning value of the handle, or `def` when it was not set
@@ -284,11 +289,16 @@ static void timed(artes_grid* g, int kind, hipStream_t s, F&& launch) {
         g->prof_ev.push_back(e);
     }
     if (g->prof_kind.size() < i + 1) g->prof_kind.resize(i + 1);
-    hipEventRecord(g->prof_ev[2 * i], s);
+    if (g->prof_start.size() < i + 1) g->prof_start.resize(i + 1);
+    int si = (int)(2 * i);
+    if (g->prof_loop && g->prof_chain && i > 0) si = (int)(2 * (i - 1) + 1);   // (the previous launch's end)
+    else hipEventRecord(g->prof_ev[2 * i], s);
     launch();
     hipEventRecord(g->prof_ev[2 * i + 1], s);
     g->prof_kind[i] = kind;
+    g->prof_start[i] = si;
     g->prof_used = i + 1;
+    g->prof_chain = true;
 }
 
 static thread_local std::string g_last_error;
@@ -869,6 +879,9 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
     int in = 0;
     long long it = 0;
     const long long max_it = tv(g, T_MAX_IT, 2000000LL);
+    g->prof_loop = true;
+    g->prof_chain = false;
+    struct LoopEnd { artes_grid* g; ~LoopEnd() { g->prof_loop = false; g->prof_chain = false; } } loop_end{g};
     for (;;) {
         SubLists L = lists(in);
         launch_trace_any<G3D>(g, gtab, wpe, trace_steps, trace_bpc, GT, R, L, stream);
@@ -887,6 +900,7 @@ static int32_t run_event_engine(artes_grid* g, const DevGrid& G, const DevRun& R
             HIP_TRY(hipMemcpy2DAsync(g->h_count, sizeof(int), cnt + cnt_at(CNT_IN0 + in, 0), CPAD * sizeof(int), sizeof(int), NSUB, hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipMemcpyAsync(h_wd, R.err + ARTES_ERR_WATCHDOG, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
             HIP_TRY(hipEventRecord(g->ev_poll, stream));
+            g->prof_chain = false;   // (the copies sit between this launch and the next)
             HIP_TRY(hipEventSynchronize(g->ev_poll));
             if (*h_wd) return fail(-5, "transport kernel watchdog fired: schedule bug, results invalid");
             long long live = 0;
@@ -1294,7 +1308,7 @@ int32_t artes_kernel_times(artes_grid* g, double* ms, uint64_t* launches) {
 #endif
     for (size_t i = 0; i < g->prof_used; i++) {
         float t = 0.0f;
-        HIP_TRY(hipEventElapsedTime(&t, g->prof_ev[2 * i], g->prof_ev[2 * i + 1]));
+        HIP_TRY(hipEventElapsedTime(&t, g->prof_ev[g->prof_start[i]], g->prof_ev[2 * i + 1]));
         ms[g->prof_kind[i]] += (double)t;
         if (launches) launches[g->prof_kind[i]] += 1;
         if (lf) fprintf(lf, "%d:%.4f ", g->prof_kind[i], t);
